@@ -1,0 +1,75 @@
+"""ctypes binding of libcse.so (the C ABI declared in include/cse.h).
+
+The product path has no CPU fallback: if the shared library (built for gfx950
+by ``__graft_entry__.build()``) is missing, every entry point raises.
+"""
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcse.so")
+
+CSE_OK = 0
+ALGO = {"NONE": -1, "SS": 0, "WIENER": 1, "MMSE": 2, "OMLSA": 3}
+NOISE = {"percentile": 0, "min_tracking": 1, "true_noise": 2}
+
+# numpy mirror of cse_cell_t (include/cse.h) — 88 bytes
+CELL_DTYPE = np.dtype([
+    ("algo", np.int32), ("hop", np.int32), ("y_offset", np.int64),
+    ("noise_offset", np.int64), ("noise_stride", np.int64), ("clean_offset", np.int64),
+    ("out_offset", np.int64), ("gain_offset", np.int64), ("param", np.float32, (8,)),
+], align=True)
+assert CELL_DTYPE.itemsize == 88
+
+EXPORTS = ("cse_version", "cse_last_error", "cse_stft", "cse_noise_workspace_bytes",
+           "cse_noise_estimate", "cse_noise_smooth", "cse_istft_norm", "cse_enhance_cells")
+
+
+def cells_per_wave(n_fft):
+    return 4 if n_fft == 512 else 2
+
+
+class CseError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libcse.so and declare prototypes (raises if it is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise CseError(f"{path} not built: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    lib = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    i32, i64, f64 = ctypes.c_int, ctypes.c_int64, ctypes.c_double
+    lib.cse_version.restype = i32
+    lib.cse_version.argtypes = []
+    lib.cse_last_error.restype = ctypes.c_char_p
+    lib.cse_last_error.argtypes = []
+    lib.cse_stft.restype = i32
+    lib.cse_stft.argtypes = [P, P, i64, i64, i32, i32, P, P, P]
+    lib.cse_noise_workspace_bytes.restype = i64
+    lib.cse_noise_workspace_bytes.argtypes = [i64, i32, i32]
+    lib.cse_noise_estimate.restype = i32
+    lib.cse_noise_estimate.argtypes = [i32, P, i64, i32, i32, f64, f64, P, P, P]
+    lib.cse_noise_smooth.restype = i32
+    lib.cse_noise_smooth.argtypes = [P, i64, i32, i32, f64, f64, P, P]
+    lib.cse_istft_norm.restype = i32
+    lib.cse_istft_norm.argtypes = [i32, i32, i64, P, P]
+    lib.cse_enhance_cells.restype = i32
+    lib.cse_enhance_cells.argtypes = [i32, i64, P, i64, P, P, P, P, P, P, P, P, P, P]
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != CSE_OK:
+        msg = load().cse_last_error().decode(errors="replace")
+        raise CseError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,134 @@
+// Shared device/host helpers for the CSE (classical speech enhancement) engine.
+// gfx950 / CDNA4 only: wave64, no CUDA shims.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+#include "../../include/cse.h"
+
+// ----------------------------------------------------------------------------
+// error reporting (thread-local message behind cse_last_error())
+// ----------------------------------------------------------------------------
+namespace cse {
+
+void set_error(const char* fmt, ...);
+
+#define CSE_CHECK_ARG(cond, ...)                 \
+    do {                                         \
+        if (!(cond)) {                           \
+            ::cse::set_error(__VA_ARGS__);       \
+            return CSE_EINVAL;                   \
+        }                                        \
+    } while (0)
+
+#define CSE_CHECK_LAUNCH(what)                                               \
+    do {                                                                     \
+        hipError_t e_ = hipGetLastError();                                   \
+        if (e_ != hipSuccess) {                                              \
+            ::cse::set_error("%s: %s", what, hipGetErrorString(e_));         \
+            return CSE_ELAUNCH;                                              \
+        }                                                                    \
+    } while (0)
+
+static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// frames of a centred STFT of an even n_fft (librosa 0.11): 1 + len // hop
+static inline int n_frames_for(int64_t len, int hop) { return 1 + (int)(len / hop); }
+
+// ----------------------------------------------------------------------------
+// complex float helpers
+// ----------------------------------------------------------------------------
+struct __attribute__((aligned(8))) cf {
+    float x, y;
+};
+
+// e^{2πi m/32}, m = 0..31 (all the compile-time rotors the kernels need)
+struct Rot32 {
+    static constexpr float c[32] = {
+        1.0f, 0.98078528040323043f, 0.92387953251128674f, 0.83146961230254524f,
+        0.70710678118654752f, 0.55557023301960218f, 0.38268343236508978f, 0.19509032201612826f,
+        0.0f, -0.19509032201612826f, -0.38268343236508978f, -0.55557023301960218f,
+        -0.70710678118654752f, -0.83146961230254524f, -0.92387953251128674f, -0.98078528040323043f,
+        -1.0f, -0.98078528040323043f, -0.92387953251128674f, -0.83146961230254524f,
+        -0.70710678118654752f, -0.55557023301960218f, -0.38268343236508978f, -0.19509032201612826f,
+        0.0f, 0.19509032201612826f, 0.38268343236508978f, 0.55557023301960218f,
+        0.70710678118654752f, 0.83146961230254524f, 0.92387953251128674f, 0.98078528040323043f};
+    static constexpr float s[32] = {
+        0.0f, 0.19509032201612826f, 0.38268343236508978f, 0.55557023301960218f,
+        0.70710678118654752f, 0.83146961230254524f, 0.92387953251128674f, 0.98078528040323043f,
+        1.0f, 0.98078528040323043f, 0.92387953251128674f, 0.83146961230254524f,
+        0.70710678118654752f, 0.55557023301960218f, 0.38268343236508978f, 0.19509032201612826f,
+        0.0f, -0.19509032201612826f, -0.38268343236508978f, -0.55557023301960218f,
+        -0.70710678118654752f, -0.83146961230254524f, -0.92387953251128674f, -0.98078528040323043f,
+        -1.0f, -0.98078528040323043f, -0.92387953251128674f, -0.83146961230254524f,
+        -0.70710678118654752f, -0.55557023301960218f, -0.38268343236508978f, -0.19509032201612826f};
+};
+
+__device__ __forceinline__ cf cmk(float x, float y) { return cf{x, y}; }
+__device__ __forceinline__ cf cadd(cf a, cf b) { return cf{a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ cf csub(cf a, cf b) { return cf{a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ cf cmul(cf a, cf b) {
+    return cf{fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x)};
+}
+__device__ __forceinline__ cf cconj(cf a) { return cf{a.x, -a.y}; }
+// multiply by +i
+__device__ __forceinline__ cf cmuli(cf a) { return cf{-a.y, a.x}; }
+__device__ __forceinline__ cf cscale(cf a, float s) { return cf{a.x * s, a.y * s}; }
+
+// ----------------------------------------------------------------------------
+// In-register inverse DFT of length 16 (sign +i): x[n] = sum_k X[k] e^{+2πi nk/16}
+// radix-4 x radix-4: k = 4k1 + k2, n = n1 + 4n2.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ void idft4(cf& a0, cf& a1, cf& a2, cf& a3) {
+    cf s02 = cadd(a0, a2), d02 = csub(a0, a2);
+    cf s13 = cadd(a1, a3), d13 = cmuli(csub(a1, a3));
+    a0 = cadd(s02, s13);
+    a2 = csub(s02, s13);
+    a1 = cadd(d02, d13);
+    a3 = csub(d02, d13);
+}
+
+// W16^m = e^{+2πi m/16} for m in [0, 9] (n1*k2 <= 9)
+__device__ __forceinline__ cf w16(int m) {
+    constexpr float c1 = 0.92387953251128674f, s1 = 0.38268343236508978f;
+    constexpr float r2 = 0.70710678118654752f;
+    switch (m) {
+        case 0: return cf{1.f, 0.f};
+        case 1: return cf{c1, s1};
+        case 2: return cf{r2, r2};
+        case 3: return cf{s1, c1};
+        case 4: return cf{0.f, 1.f};
+        case 5: return cf{-s1, c1};
+        case 6: return cf{-r2, r2};
+        case 7: return cf{-c1, s1};
+        case 8: return cf{-1.f, 0.f};
+        default: return cf{-c1, -s1};  // 9
+    }
+}
+
+__device__ __forceinline__ void idft16(cf (&v)[16]) {
+    // step 1: for each k2, DFT4 over k1 of v[4k1+k2] -> index n1 (stored in place)
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) idft4(v[k2], v[4 + k2], v[8 + k2], v[12 + k2]);
+    // now v[4*n1 + k2] holds A[n1][k2]; twiddle by W16^{n1*k2}
+#pragma unroll
+    for (int n1 = 1; n1 < 4; ++n1)
+#pragma unroll
+        for (int k2 = 1; k2 < 4; ++k2) v[4 * n1 + k2] = cmul(v[4 * n1 + k2], w16(n1 * k2));
+    // step 2: for each n1, DFT4 over k2 -> index n2; result x[n1 + 4n2]
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1) idft4(v[4 * n1], v[4 * n1 + 1], v[4 * n1 + 2], v[4 * n1 + 3]);
+    // v[4*n1 + n2] = x[n1 + 4 n2]: transpose 4x4 to natural order
+    cf t[16];
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1)
+#pragma unroll
+        for (int n2 = 0; n2 < 4; ++n2) t[n1 + 4 * n2] = v[4 * n1 + n2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = t[i];
+}
+
+}  // namespace cse

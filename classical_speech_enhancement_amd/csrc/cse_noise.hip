@@ -1,0 +1,339 @@
+// Noise-PSD estimators (Code/noise_estimation.py) on device, fp64 math.
+//
+//   PercentileNoiseEstimator.estimate   :20-56   -> frame_energy + select_quiet + bin_stats
+//   MinTrackingNoiseEstimator.estimate  :64-95   -> bin_stats(median) + iir + min_filter
+//   TrueNoiseEstimator.estimate         :115-155 -> floor_cast on |STFT(noisy-clean)|^2
+//   _simple_noise_estimate              :226-232 -> bin_stats(simple) when T < 5
+//   noise smoothing (mmse.py:48-54, advanced_mmse.py:60-66) -> smooth_kernel
+//
+// These run once per (signal, n_fft, hop) group and are amortised over the
+// hundreds of grid cells that share the group, so they favour exactness
+// (fp64, full sorts reproducing np.percentile / np.median) over speed.
+#include "cse_common.hpp"
+
+#include <math.h>
+
+namespace cse {
+
+constexpr int kMaxSortFrames = 8192;  // LDS bitonic sort capacity (T <= 8192)
+
+__device__ __forceinline__ bool key_less(double a, int ia, double b, int ib) {
+    return a < b || (a == b && ia < ib);
+}
+
+// ascending bitonic sort of n2 (power of two) keys (+ optional indices) in LDS
+__device__ void bitonic_sort(double* key, int* idx, int n2) {
+    for (int k = 2; k <= n2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const bool up = (i & k) == 0;
+                    const int ii = idx ? idx[i] : i, il = idx ? idx[l] : l;
+                    const bool gt = key_less(key[l], il, key[i], ii);
+                    if (gt == up) {
+                        double tk = key[i];
+                        key[i] = key[l];
+                        key[l] = tk;
+                        if (idx) {
+                            int ti = idx[i];
+                            idx[i] = idx[l];
+                            idx[l] = ti;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+static int next_pow2(int n) {
+    int p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+// np.percentile(sorted[0:n], pct) with method='linear' (numpy 2.x _quantile/_lerp)
+__device__ double lerp_percentile(const double* s, int n, double q) {
+    const double virt = (double)(n - 1) * q;
+    double prev_f = floor(virt);
+    int prev, next;
+    if (virt >= (double)(n - 1)) {
+        prev = next = n - 1;
+        prev_f = -1.0;  // numpy sets previous_indexes = -1 here; gamma uses it
+    } else if (virt < 0.0) {
+        prev = next = 0;
+        prev_f = 0.0;
+    } else {
+        prev = (int)prev_f;
+        next = prev + 1;
+    }
+    const double gamma = virt - prev_f;
+    const double a = s[prev], b = s[next];
+    const double diff = b - a;
+    if (gamma >= 0.5) return b - diff * (1.0 - gamma);
+    return a + diff * gamma;
+}
+
+// mean_b log(max(P[t][b], eps)) per frame
+__global__ void frame_energy_kernel(const double* __restrict__ P, int T, int B, double eps,
+                                    double* __restrict__ energy) {
+    __shared__ double part[256];
+    const int t = blockIdx.x;
+    const int64_t sig = blockIdx.y;
+    const double* row = P + (sig * T + t) * (int64_t)B;
+    double s = 0.0;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) s += log(fmax(row[b], eps));
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) energy[sig * T + t] = part[0] / (double)B;
+}
+
+// k quietest frames: argsort(energy)[:k] (ties by frame index)
+__global__ void select_quiet_kernel(const double* __restrict__ energy, int T, int n2, int k,
+                                    int* __restrict__ sel) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double* key = (double*)smem;
+    int* idx = (int*)(key + n2);
+    const int64_t sig = blockIdx.x;
+    for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+        key[i] = i < T ? energy[sig * T + i] : INFINITY;
+        idx[i] = i;
+    }
+    __syncthreads();
+    bitonic_sort(key, idx, n2);
+    for (int i = threadIdx.x; i < k; i += blockDim.x) sel[sig * (int64_t)T + i] = idx[i];
+}
+
+enum { STATS_MEDIAN = 0, STATS_PERCENTILE = 1, STATS_SIMPLE = 2 };
+
+// per (bin, signal): median over all frames (-> med), and optionally the
+// percentile over the selected quiet frames (-> N) or the T<5 simple estimate.
+__global__ void bin_stats_kernel(const double* __restrict__ P, int T, int B, int n2_all,
+                                 int mode, const int* __restrict__ sel, int k, int n2_sel,
+                                 double q, double floor_rel, double eps,
+                                 double* __restrict__ med, float* __restrict__ N,
+                                 int broadcast_T) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double* s = (double*)smem;
+    const int b = blockIdx.x;
+    const int64_t sig = blockIdx.y;
+    const double* Ps = P + sig * (int64_t)T * B + b;
+    double median = 0.0;
+    if (mode != STATS_SIMPLE) {
+        for (int i = threadIdx.x; i < n2_all; i += blockDim.x)
+            s[i] = i < T ? Ps[(int64_t)i * B] : INFINITY;
+        __syncthreads();
+        bitonic_sort(s, nullptr, n2_all);
+        median = (T & 1) ? s[T / 2] : (s[T / 2 - 1] + s[T / 2]) / 2.0;
+        if (threadIdx.x == 0 && med) med[sig * B + b] = median;
+        __syncthreads();
+    }
+    if (mode == STATS_MEDIAN) return;
+    double est;
+    if (mode == STATS_PERCENTILE) {
+        for (int i = threadIdx.x; i < n2_sel; i += blockDim.x)
+            s[i] = i < k ? Ps[(int64_t)sel[sig * (int64_t)T + i] * B] : INFINITY;
+        __syncthreads();
+        bitonic_sort(s, nullptr, n2_sel);
+        est = fmax(lerp_percentile(s, k, q), floor_rel * median);
+    } else {  // simple: mean (T < 2) or 25th percentile over all frames
+        for (int i = threadIdx.x; i < n2_all; i += blockDim.x)
+            s[i] = i < T ? Ps[(int64_t)i * B] : INFINITY;
+        __syncthreads();
+        bitonic_sort(s, nullptr, n2_all);
+        est = (T < 2) ? s[0] : lerp_percentile(s, T, 0.25);
+    }
+    const float v = (float)fmax(est, eps);
+    if (broadcast_T) {
+        for (int t = threadIdx.x; t < T; t += blockDim.x) N[(sig * T + t) * (int64_t)B + b] = v;
+    } else if (threadIdx.x == 0) {
+        N[sig * B + b] = v;
+    }
+}
+
+// S_t = a*S_{t-1} + (1-a)*P_t (noise_estimation.py:78-82), numpy evaluation order
+__global__ void iir_kernel(const double* __restrict__ P, int T, int B, double a,
+                           double* __restrict__ S) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t sig = blockIdx.y;
+    if (b >= B) return;
+    const double* Ps = P + sig * (int64_t)T * B + b;
+    double* Ss = S + sig * (int64_t)T * B + b;
+    double s = Ps[0];
+    Ss[0] = s;
+    const double c = 1.0 - a;
+    for (int t = 1; t < T; ++t) {
+        s = __dadd_rn(__dmul_rn(a, s), __dmul_rn(c, Ps[(int64_t)t * B]));
+        Ss[(int64_t)t * B] = s;
+    }
+}
+
+// minimum_filter1d(S, size=w, mode='nearest') then floors (noise_estimation.py:86-95)
+__global__ void min_filter_kernel(const double* __restrict__ S, int T, int B, int half,
+                                  const double* __restrict__ med, double eps,
+                                  float* __restrict__ N) {
+    const int t = blockIdx.x;
+    const int64_t sig = blockIdx.y;
+    const int lo = t - half < 0 ? 0 : t - half;
+    const int hi = t + half > T - 1 ? T - 1 : t + half;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) {
+        const double* Ss = S + sig * (int64_t)T * B + b;
+        double m = Ss[(int64_t)lo * B];
+        for (int u = lo + 1; u <= hi; ++u) m = fmin(m, Ss[(int64_t)u * B]);
+        const double v = fmax(fmax(m, 0.01 * med[sig * B + b]), eps);
+        N[(sig * T + t) * (int64_t)B + b] = (float)v;
+    }
+}
+
+__global__ void floor_cast_kernel(const double* __restrict__ P, int64_t n, double eps,
+                                  float* __restrict__ N) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) N[i] = (float)fmax(P[i], eps);
+}
+
+__global__ void smooth_kernel(const float* __restrict__ N, int T, int B, double mu,
+                              double pre_eps, float* __restrict__ out) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t sig = blockIdx.y;
+    if (b >= B) return;
+    const float* Ns = N + sig * (int64_t)T * B + b;
+    float* Os = out + sig * (int64_t)T * B + b;
+    double s = (double)Ns[0];
+    if (pre_eps > 0.0) s = fmax(s, pre_eps);
+    Os[0] = (float)s;
+    const double c = 1.0 - mu;
+    for (int t = 1; t < T; ++t) {
+        double n = (double)Ns[(int64_t)t * B];
+        if (pre_eps > 0.0) n = fmax(n, pre_eps);
+        s = __dadd_rn(__dmul_rn(mu, s), __dmul_rn(c, n));
+        Os[(int64_t)t * B] = (float)s;
+    }
+}
+
+struct Workspace {
+    double* energy;  // [n_sig][T]
+    int* sel;        // [n_sig][T]
+    double* med;     // [n_sig][B]
+    double* S;       // [n_sig][T][B]
+};
+
+static int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+static Workspace carve(void* ws, int64_t n_sig, int T, int B) {
+    unsigned char* p = (unsigned char*)ws;
+    Workspace w;
+    w.energy = (double*)p;
+    p += align256(n_sig * (int64_t)T * 8);
+    w.sel = (int*)p;
+    p += align256(n_sig * (int64_t)T * 4);
+    w.med = (double*)p;
+    p += align256(n_sig * (int64_t)B * 8);
+    w.S = (double*)p;
+    return w;
+}
+
+// (k, percentile) exactly as noise_estimation.py:29-41
+static void quiet_count(int T, double pct_in, int* k_out, double* pct_out) {
+    int min_frames = 10;
+    double pct = pct_in;
+    if (T < 30) {
+        min_frames = (T / 4 > 2) ? T / 4 : 2;
+        const int target = ((int)(T * 0.15) > 3) ? (int)(T * 0.15) : 3;
+        pct = 100.0 * target / T;
+        if (pct > 50.0) pct = 50.0;
+    }
+    int k = (int)ceil((double)T * (pct / 100.0));
+    if (k < min_frames) k = min_frames;
+    int cap = (int)ceil((double)T * 0.30);
+    if (cap < 1) cap = 1;
+    if (k > cap) k = cap;
+    if (k > T) k = T;
+    *k_out = k;
+    *pct_out = pct;
+}
+
+}  // namespace cse
+
+using namespace cse;
+
+extern "C" int64_t cse_noise_workspace_bytes(int64_t n_sig, int T, int B) {
+    return align256(n_sig * (int64_t)T * 8) + align256(n_sig * (int64_t)T * 4) +
+           align256(n_sig * (int64_t)B * 8) + align256(n_sig * (int64_t)T * B * 8);
+}
+
+extern "C" int cse_noise_estimate(int method, const double* P, int64_t n_sig, int T, int B,
+                                  double percentile, double eps, float* N, void* workspace,
+                                  cse_stream_t stream) {
+    hipStream_t s = (hipStream_t)stream;
+    CSE_CHECK_ARG(P && N, "cse_noise_estimate: NULL P or N");
+    CSE_CHECK_ARG(n_sig > 0 && n_sig < 65536 && T >= 1 && B >= 2,
+                  "cse_noise_estimate: bad shape n_sig=%lld T=%d B=%d", (long long)n_sig, T, B);
+    CSE_CHECK_ARG(T <= kMaxSortFrames, "cse_noise_estimate: T=%d > %d frames unsupported", T,
+                  kMaxSortFrames);
+    if (method == CSE_NOISE_TRUE) {
+        const int64_t n = n_sig * (int64_t)T * B;
+        hipLaunchKernelGGL(floor_cast_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, s, P, n, eps,
+                           N);
+        CSE_CHECK_LAUNCH("cse_noise_estimate(true)");
+        return CSE_OK;
+    }
+    CSE_CHECK_ARG(method == CSE_NOISE_PERCENTILE || method == CSE_NOISE_MIN_TRACKING,
+                  "Unbekannte Methode: %d", method);
+    CSE_CHECK_ARG(workspace != nullptr, "cse_noise_estimate: workspace is NULL");
+    Workspace w = carve(workspace, n_sig, T, B);
+    const int n2_all = next_pow2(T);
+    const size_t lds_all = (size_t)n2_all * sizeof(double);
+    dim3 grid_bins(B, (unsigned)n_sig);
+    if (T < 5) {  // noise_estimation.py:194-195
+        hipLaunchKernelGGL(bin_stats_kernel, grid_bins, dim3(256), lds_all, s, P, T, B, n2_all,
+                           (int)STATS_SIMPLE, (const int*)nullptr, 0, 0, 0.0, 0.0, eps,
+                           (double*)nullptr, N, method == CSE_NOISE_MIN_TRACKING ? 1 : 0);
+        CSE_CHECK_LAUNCH("cse_noise_estimate(simple)");
+        return CSE_OK;
+    }
+    if (method == CSE_NOISE_PERCENTILE) {
+        int k;
+        double pct;
+        quiet_count(T, percentile, &k, &pct);
+        const int n2_sel = next_pow2(k);
+        hipLaunchKernelGGL(frame_energy_kernel, dim3(T, (unsigned)n_sig), dim3(256), 0, s, P, T,
+                           B, eps, w.energy);
+        hipLaunchKernelGGL(select_quiet_kernel, dim3((unsigned)n_sig), dim3(1024),
+                           (size_t)n2_all * 12, s, (const double*)w.energy, T, n2_all, k, w.sel);
+        hipLaunchKernelGGL(bin_stats_kernel, grid_bins, dim3(256), lds_all, s, P, T, B, n2_all,
+                           (int)STATS_PERCENTILE, (const int*)w.sel, k, n2_sel, pct / 100.0,
+                           0.02, eps, w.med, N, 0);
+        CSE_CHECK_LAUNCH("cse_noise_estimate(percentile)");
+        return CSE_OK;
+    }
+    // min tracking
+    const double a = fmax(0.8, fmin(0.95, 1.0 - 5.0 / (double)T));
+    int win = T < 50 ? T : 50;  // min(max(3, 50), T)
+    if (win % 2 == 0) win += 1;
+    hipLaunchKernelGGL(bin_stats_kernel, grid_bins, dim3(256), lds_all, s, P, T, B, n2_all,
+                       (int)STATS_MEDIAN, (const int*)nullptr, 0, 0, 0.0, 0.0, eps, w.med,
+                       (float*)nullptr, 0);
+    hipLaunchKernelGGL(iir_kernel, dim3(ceil_div(B, 64), (unsigned)n_sig), dim3(64), 0, s, P, T, B,
+                       a, w.S);
+    hipLaunchKernelGGL(min_filter_kernel, dim3(T, (unsigned)n_sig), dim3(256), 0, s,
+                       (const double*)w.S, T, B, win / 2, (const double*)w.med, eps, N);
+    CSE_CHECK_LAUNCH("cse_noise_estimate(min_tracking)");
+    return CSE_OK;
+}
+
+extern "C" int cse_noise_smooth(const float* N, int64_t n_sig, int T, int B, double mu,
+                                double pre_eps, float* out, cse_stream_t stream) {
+    CSE_CHECK_ARG(N && out, "cse_noise_smooth: NULL pointer");
+    CSE_CHECK_ARG(n_sig > 0 && n_sig < 65536 && T >= 1 && B >= 1, "cse_noise_smooth: bad shape");
+    const double m = fmin(fmax(mu, 0.0), 0.9999);
+    hipLaunchKernelGGL(smooth_kernel, dim3(ceil_div(B, 64), (unsigned)n_sig), dim3(64), 0,
+                       (hipStream_t)stream, N, T, B, m, pre_eps, out);
+    CSE_CHECK_LAUNCH("cse_noise_smooth");
+    return CSE_OK;
+}

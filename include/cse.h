@@ -1,0 +1,155 @@
+/*
+ * cse.h — C ABI of libcse.so, the MI355X (gfx950) engine for the STFT
+ * frame-gain path of Katja39/Classical_Speech_Enhancement.
+ *
+ * The reference has no FFI: its seams are Python plugins:
+ *   alg_fn(noisy_audio, sr, **params) -> ndarray   registered at
+ *     Code/speech_enhancement_comparison.py:395-401, called via
+ *     algorithm_wrapper :282-292 from the grid loop :156-226;
+ *   NoiseEstimator.estimate(power, **kw)          Code/noise_estimation.py:6-9,
+ *     selected by _create_estimator :215-223.
+ * Each entry point below replaces the numeric core behind one of those
+ * seams; the Python package mirrors the plugin signatures on top of it
+ * (see INTEGRATION.md for the ctypes binding).
+ *
+ * Conventions
+ *   - Every pointer is CALLER-OWNED DEVICE memory (hipMalloc / torch tensor).
+ *     The library allocates nothing; every call is enqueued on `stream` and
+ *     returns immediately (asynchronous, reentrant per stream).
+ *   - Return value: CSE_OK (0) or a negative CSE_E* code; cse_last_error()
+ *     returns a thread-local message for the last failure.
+ *   - Layouts are frame-major: spectra are [signal][frame][bin] with
+ *     bins = n_fft/2 + 1 contiguous; complex values are interleaved
+ *     (re, im) float pairs.
+ *   - Per-cell numerical failure (non-finite output) is reported through the
+ *     `finite` output, never as a status code — it mirrors the reference's
+ *     "skip this cell" semantics (speech_enhancement_comparison.py:102-103).
+ */
+#ifndef CSE_H_
+#define CSE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* cse_stream_t; /* == hipStream_t */
+
+enum {
+    CSE_OK = 0,
+    CSE_EINVAL = -1,  /* bad argument / unsupported shape */
+    CSE_ELAUNCH = -2, /* HIP launch failure */
+};
+
+/* algorithms (cse_cell_t.algo) */
+enum {
+    CSE_ALGO_NONE = -1, /* padding slot: computes nothing, writes nothing */
+    CSE_ALGO_SS = 0,    /* spectral_subtractor.py:6-65   param: alpha, beta            */
+    CSE_ALGO_WIENER = 1,/* wiener_filter.py:7-95         param: alpha, gain_floor      */
+    CSE_ALGO_MMSE = 2,  /* mmse.py:6-120                 param: alpha, ksi_min, gain_min, gain_max */
+    CSE_ALGO_OMLSA = 3, /* advanced_mmse.py:7-136        param: alpha, ksi_min, gain_floor, q, v_max */
+};
+
+/* noise-PSD estimators (noise_estimation.py) */
+enum {
+    CSE_NOISE_PERCENTILE = 0,   /* :11-56  static [B]            */
+    CSE_NOISE_MIN_TRACKING = 1, /* :59-107 time-varying [T][B]   */
+    CSE_NOISE_TRUE = 2,         /* :109-155 time-varying [T][B]  */
+};
+
+/*
+ * One grid cell = one (signal group, noise PSD, algorithm, parameter set).
+ * Cells are processed CSE_CELLS_PER_WAVE(n_fft) at a time by one wavefront;
+ * all cells of such a slot group must have the same `hop` (pad with
+ * CSE_ALGO_NONE slots).  Cells of one slot group that also share `y_offset`
+ * and `noise_offset` share their global loads (fastest).
+ */
+typedef struct cse_cell {
+    int32_t algo;          /* CSE_ALGO_* */
+    int32_t hop;           /* hop length; 128 or 256 */
+    int64_t y_offset;      /* offset (in complex elements) of this cell's spectrum Y[T][B] */
+    int64_t noise_offset;  /* offset (floats) of this cell's noise PSD */
+    int64_t noise_stride;  /* floats between frames of the noise PSD: 0 = static [B], B = [T][B] */
+    int64_t clean_offset;  /* offset (floats) of the clean reference for the SNR, or -1 */
+    int64_t out_offset;    /* offset (floats) of this cell's output waveform in y_out, or -1 */
+    int64_t gain_offset;   /* offset (floats) of this cell's gain matrix G[T][B] in g_out, or -1 */
+    float param[8];        /* algorithm parameters, order as in the CSE_ALGO_* comments */
+} cse_cell_t;              /* 88 bytes */
+
+#define CSE_CELLS_PER_WAVE(n_fft) ((n_fft) == 512 ? 4 : 2)
+
+/* Library identity. */
+int cse_version(void);
+const char* cse_last_error(void);
+
+/*
+ * Centred, reflect-padded, periodic-Hann STFT (librosa 0.11 `stft` as called
+ * at spectral_subtractor.py:25, wiener_filter.py:35, mmse.py:29,
+ * advanced_mmse.py:39 and noise_estimation.py:184-188, :136-144), computed in
+ * fp64.  x: [n_sig][len] f64.  If x_sub != NULL the transform is taken of
+ * (x - x_sub) (TrueNoise, noise_estimation.py:133).  T = 1 + len/hop.
+ * Outputs (either may be NULL): Y [n_sig][T][B] complex64, P [n_sig][T][B] f64 = |Y|^2.
+ */
+int cse_stft(const double* x, const double* x_sub, int64_t n_sig, int64_t len, int n_fft,
+             int hop, float* Y, double* P, cse_stream_t stream);
+
+/* Workspace bytes needed by cse_noise_estimate for one call. */
+int64_t cse_noise_workspace_bytes(int64_t n_sig, int T, int B);
+
+/*
+ * Noise-PSD estimators on P [n_sig][T][B] f64 (noise_estimation.py):
+ *   CSE_NOISE_PERCENTILE   -> N [n_sig][B]   (PercentileNoiseEstimator :20-56,
+ *                             or _simple_noise_estimate :226-232 when T < 5)
+ *   CSE_NOISE_MIN_TRACKING -> N [n_sig][T][B] (MinTrackingNoiseEstimator :64-95,
+ *                             or the static T < 5 fallback, broadcast over T)
+ *   CSE_NOISE_TRUE         -> N [n_sig][T][B] = max(P, eps) where P is the
+ *                             power of STFT(noisy - clean) (:135-147)
+ * percentile is ignored except for CSE_NOISE_PERCENTILE.  N is f32.
+ * workspace: >= cse_noise_workspace_bytes(n_sig, T, B) bytes of device memory.
+ */
+int cse_noise_estimate(int method, const double* P, int64_t n_sig, int T, int B,
+                       double percentile, double eps, float* N, void* workspace,
+                       cse_stream_t stream);
+
+/*
+ * First-order IIR smoothing of a time-varying noise PSD over frames
+ * (mmse.py:48-54, advanced_mmse.py:60-66): out_0 = N_0,
+ * out_t = mu*out_{t-1} + (1-mu)*N_t with mu = clip(mu, 0, 0.9999), after an
+ * optional floor N <- max(N, pre_eps) (pass pre_eps <= 0 for none).  fp64 math.
+ */
+int cse_noise_smooth(const float* N, int64_t n_sig, int T, int B, double mu,
+                     double pre_eps, float* out, cse_stream_t stream);
+
+/*
+ * 1 / window-sum-square of the ISTFT (librosa 0.11 istft normalisation) for a
+ * centred signal of `len` samples; entries where the sum is <= DBL_MIN are 1.
+ * out: [len] f32.
+ */
+int cse_istft_norm(int n_fft, int hop, int64_t len, float* out, cse_stream_t stream);
+
+/*
+ * THE HOT PATH.  For every cell: the per-frame gain recursion of its algorithm
+ * (decision-directed a-priori SNR, serial over frames), S = Y*G (SS: noisy
+ * phase), inverse real FFT, periodic-Hann synthesis window, overlap-add,
+ * window-sum-square normalisation (librosa istft, length = len), and the
+ * per-cell score reductions:
+ *   sse[c]    = sum_n (clean[n] - clip(y[n], -1, 1))^2   (f64; if clean_offset >= 0)
+ *   finite[c] = 1 if every y[n] is finite
+ * Optional outputs: y_out (the enhanced waveform, f32, [len] at out_offset)
+ * and g_out (the gain matrix, f32 [T][B] at gain_offset).
+ * inv_wss128 / inv_wss256: cse_istft_norm tables for hop 128 / 256 (each may
+ * be NULL if no cell uses that hop).
+ * n_fft in {512, 1024}; hop in {128, 256}.
+ */
+int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
+                      const float* Y, const float* noise, const float* clean,
+                      const float* inv_wss128, const float* inv_wss256,
+                      float* y_out, float* g_out, double* sse, uint8_t* finite,
+                      cse_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CSE_H_ */

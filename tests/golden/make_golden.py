@@ -1,0 +1,241 @@
+"""Generate the golden fixtures under tests/golden/ — DEV CONTAINER ONLY.
+
+Imports the UNMODIFIED reference modules from /root/reference/Code (read-only)
+with a ``librosa`` shim (the oracle's own restatement of librosa 0.11
+stft/istft/fix_length, since librosa is not installed here) and stub modules
+for the I/O / metric libraries the driver imports but the hot path never
+calls (soundfile, pystoi, pesq).  Runs the reference functions on seeded
+synthetic inputs and stores inputs + outputs as .npz fixtures.
+
+What the fixtures pin: the reference's own algorithm, estimator, grid and
+finalize/SNR code (fp64).  What they do NOT pin: librosa itself (the shim is
+ours) — see DESIGN.md §Oracle.
+
+The reference never travels: only the .npz data written here is committed.
+
+    python tests/golden/make_golden.py            # writes tests/golden/*.npz
+"""
+
+import os
+import sys
+import types
+import wave
+
+import numpy as np
+
+REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+REF = "/root/reference/Code"
+OUT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from oracle import stft_ref  # noqa: E402
+from classical_speech_enhancement_amd.synth import make_pair  # noqa: E402
+
+
+def install_shims():
+    lib = types.ModuleType("librosa")
+    lib.stft = stft_ref.stft
+    lib.istft = stft_ref.istft
+    util = types.ModuleType("librosa.util")
+    util.fix_length = stft_ref.fix_length
+    lib.util = util
+
+    def _no_resample(*a, **k):
+        raise RuntimeError("librosa.resample is not restated (soxr)")
+    lib.resample = _no_resample
+    lib.load = _no_resample
+    sys.modules["librosa"] = lib
+    sys.modules["librosa.util"] = util
+    sf = types.ModuleType("soundfile")
+    sf.write = lambda *a, **k: None
+    sys.modules["soundfile"] = sf
+    pystoi = types.ModuleType("pystoi")
+    pystoi.stoi = lambda *a, **k: (_ for _ in ()).throw(RuntimeError("pystoi absent"))
+    sys.modules["pystoi"] = pystoi
+    pesq = types.ModuleType("pesq")
+    pesq.pesq = lambda *a, **k: (_ for _ in ()).throw(RuntimeError("pesq absent"))
+    sys.modules["pesq"] = pesq
+    sys.path.insert(0, REF)
+
+
+def ref_modules():
+    install_shims()
+    import spectral_subtractor
+    import wiener_filter
+    import mmse
+    import advanced_mmse
+    import noise_estimation
+    import parameter_ranges
+    import speech_enhancement_comparison as sec
+    import evaluation_metrics as em
+    return dict(ss=spectral_subtractor.spectral_subtraction,
+                wiener=wiener_filter.wiener_filter, mmse=mmse.mmse,
+                omlsa=advanced_mmse.advanced_mmse,
+                noise=noise_estimation.noise_estimation, pr=parameter_ranges,
+                sec=sec, em=em)
+
+
+# one representative cell per algorithm (mid-grid values of parameter_ranges.py)
+CELLS = {
+    "ss": dict(alpha=2.0, beta=0.005),
+    "wiener": dict(alpha=0.95, gain_floor=0.05),
+    "mmse": dict(alpha=0.98, ksi_min=0.01, gain_min=0.05, gain_max=1.0),
+    "omlsa": dict(alpha=0.9, ksi_min=0.005, gain_floor=0.1, noise_mu=0.95, q=0.4),
+}
+EPS = {"ss": 1e-10, "wiener": 1e-10, "mmse": 1e-12, "omlsa": 1e-10}
+
+
+def gen_algorithms(R):
+    """Fixture 1: every algorithm x method x (n_fft, hop) on a 0.75-s pair.
+
+    The clean input is stored as float32 (it only feeds true_noise, exactly as
+    stored here); the noisy input is stored in full precision.
+    """
+    clean, noisy = make_pair(7, seconds=0.75)
+    clean = clean.astype(np.float32).astype(np.float64)
+    out = {"clean": clean.astype(np.float32), "noisy": noisy, "synth": np.asarray([7, 0.75])}
+    for alg, base in CELLS.items():
+        for method in ("percentile", "min_tracking", "true_noise"):
+            for n_fft, hop in ((512, 128), (1024, 256), (512, 256), (1024, 128)):
+                full = (n_fft, hop) in ((512, 128), (1024, 256))
+                pcts = (10.0, 20.0) if (method == "percentile" and full) else (
+                    (20.0,) if method == "percentile" else (10.0,))
+                if not full and method == "true_noise":
+                    continue
+                for pct in pcts:
+                    kw = dict(base, n_fft=n_fft, hop_length=hop,
+                              noise_percentile=pct, noise_method=method)
+                    if method == "true_noise":
+                        kw["clean_audio"] = clean
+                    y = R[alg](noisy, 16000, **kw)
+                    key = f"{alg}|{method}|{n_fft}|{hop}|{int(pct)}"
+                    out["y|" + key] = np.asarray(y, dtype=np.float64)
+                    if alg in ("ss", "mmse") and full:  # two eps values cover all four algs
+                        N = R["noise"](noisy, sr=16000, n_fft=n_fft, hop_length=hop,
+                                       win_length=n_fft, percentile=pct, method=method,
+                                       clean_audio=clean, eps=EPS[alg])
+                        out[f"N|{method}|{n_fft}|{hop}|{int(pct)}|{EPS[alg]:g}"] = N
+    np.savez_compressed(os.path.join(OUT, "algorithms_0p75s.npz"), **out)
+    print("algorithms_0p75s.npz", len(out))
+
+
+def _sha(x):
+    import hashlib
+    return np.asarray(hashlib.sha256(np.ascontiguousarray(x, dtype=np.float64).tobytes()).hexdigest())
+
+
+def gen_config1(R):
+    """Fixture 2: BASELINE config 1 — SS 512/128 true_noise on a 10-s pair."""
+    clean, noisy = make_pair(0, seconds=10.0)
+    kw = dict(alpha=1.5, beta=0.001, n_fft=512, hop_length=128,
+              noise_percentile=10.0, noise_method="true_noise", clean_audio=clean)
+    y = R["ss"](noisy, 16000, **kw)
+    np.savez_compressed(os.path.join(OUT, "config1_ss_true_noise_10s.npz"),
+                        clean_sha=_sha(clean), noisy_sha=_sha(noisy), synth=np.asarray([0, 10.0]),
+                        y=np.asarray(y, dtype=np.float64),
+                        snr=R["em"].calculate_snr(clean, np.clip(y, -1, 1)))
+    print("config1 done")
+
+
+def gen_grid_snr(R):
+    """Fixture 3: full-grid per-cell finalize+SNR table for one short pair."""
+    import itertools
+    clean, noisy = make_pair(3, seconds=0.5)
+    sec = R["sec"]
+    out = {"clean": clean, "noisy": noisy}
+    for alg, ranges in (("ss", R["pr"].param_ranges_ss), ("mmse", R["pr"].param_ranges_mmse),
+                        ("wiener", R["pr"].param_ranges_wiener),
+                        ("omlsa", R["pr"].param_ranges_omlsa)):
+        names = list(ranges.keys())
+        snr, lag0 = [], []
+        for combo in itertools.product(*ranges.values()):
+            p = dict(zip(names, combo))
+            y = np.asarray(R[alg](noisy, 16000, **p), dtype=np.float64)
+            e = sec.finalize_enhanced(y, clean, 16000, do_align=True)
+            snr.append(np.nan if e is None else R["em"].calculate_snr(clean, e))
+            lag0.append(R["em"].calculate_snr(clean, np.clip(y, -1, 1)))
+        out[f"snr|{alg}"] = np.asarray(snr)
+        out[f"snr_lag0|{alg}"] = np.asarray(lag0)
+        print(alg, len(snr))
+    np.savez_compressed(os.path.join(OUT, "grid_snr_0p5s.npz"), **out)
+
+
+def gen_short(R):
+    """Fixture 4: short-clip edge cases (T<5 fallback and T<30 percentile)."""
+    out = {}
+    for tag, n in (("t3", 300), ("t20", 2500)):
+        clean, noisy = make_pair(11, seconds=n / 16000.0)
+        out[f"noisy|{tag}"] = noisy
+        out[f"clean|{tag}"] = clean
+        for alg, base in CELLS.items():
+            for method in ("percentile", "min_tracking"):
+                y = R[alg](noisy, 16000, **dict(base, n_fft=512, hop_length=128,
+                                                noise_percentile=20.0, noise_method=method))
+                out[f"y|{tag}|{alg}|{method}"] = np.asarray(y, dtype=np.float64)
+    np.savez_compressed(os.path.join(OUT, "short_clips.npz"), **out)
+    print("short done")
+
+
+def _read_wav(path):
+    with wave.open(path) as w:
+        assert w.getsampwidth() == 2 and w.getnchannels() == 1
+        sr = w.getframerate()
+        x = np.frombuffer(w.readframes(w.getnframes()), dtype="<i2").astype(np.float64) / 32768.0
+    return x, sr
+
+
+def gen_presentation(R):
+    """Loose real-speech fixtures from Document/Presentation.
+
+    48-kHz inputs are brought to 16 kHz with scipy resample_poly(1, 3) — a
+    stand-in for librosa's soxr resampler (unavailable) — then the
+    reference's prepare_pair alignment runs; the expected outputs are the
+    reference's committed 16-kHz PCM16 WAVs.
+    """
+    from scipy.signal import resample_poly
+    sec = R["sec"]
+    base = "/root/reference/Document/Presentation"
+    cases = {
+        "p257_090": ("lowSTOI_SpectralSubtraction_p257_090", "spectralSubtractor", {
+            "pesq": dict(alpha=1.5, beta=0.001, n_fft=512, hop_length=128,
+                         noise_percentile=10.0, noise_method="true_noise"),
+            "stoi": dict(alpha=1.0, beta=0.001, n_fft=1024, hop_length=256,
+                         noise_percentile=10.0, noise_method="true_noise")}),
+        "p257_135": ("wiener_p257_135", "wiener", {
+            "pesq": dict(alpha=0.95, gain_floor=0.2, n_fft=512, hop_length=128,
+                         noise_percentile=10.0, noise_method="min_tracking")}),
+    }
+    out = {}
+    for stem, (d, alg, variants) in cases.items():
+        c48, _ = _read_wav(f"{base}/{d}/{stem}_clean.wav")
+        n48, _ = _read_wav(f"{base}/{d}/{stem}_noisy.wav")
+        c16 = resample_poly(c48, 1, 3)
+        n16 = resample_poly(n48, 1, 3)
+        L = min(len(c16), len(n16))
+        c16, n16 = c16[:L], n16[:L]
+        n16 = sec.match_length(sec.align_to_reference(c16, n16, 16000), L)
+        out[f"clean|{stem}"] = c16.astype(np.float32)
+        out[f"noisy|{stem}"] = n16.astype(np.float32)
+        for var, params in variants.items():
+            exp, sr = _read_wav(f"{base}/{d}/{stem}_{alg}_optimized_{var}.wav")
+            assert sr == 16000
+            out[f"expected|{stem}|{var}"] = (exp * 32768.0).astype(np.int16)
+            for k, v in params.items():
+                out[f"param|{stem}|{var}|{k}"] = np.asarray(v)
+    np.savez_compressed(os.path.join(OUT, "presentation_wavs.npz"), **out)
+    print("presentation done")
+
+
+if __name__ == "__main__":
+    R = ref_modules()
+    which = sys.argv[1:] or ["algorithms", "config1", "short", "presentation", "grid"]
+    if "algorithms" in which:
+        gen_algorithms(R)
+    if "config1" in which:
+        gen_config1(R)
+    if "short" in which:
+        gen_short(R)
+    if "presentation" in which:
+        gen_presentation(R)
+    if "grid" in which:
+        gen_grid_snr(R)

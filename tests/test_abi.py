@@ -1,0 +1,78 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol that
+include/cse.h declares, and rejects bad arguments with status codes."""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from classical_speech_enhancement_amd import _lib
+
+HEADER = os.path.join(os.path.dirname(__file__), "..", "include", "cse.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(cse_[a-z0-9_]+)\s*\(", text)) - {"cse_cell"})
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build()
+    return _lib.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    names = _declared()
+    assert set(names) == set(_lib.EXPORTS)
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_version_and_error_channel(lib):
+    assert lib.cse_version() == 1
+    rc = lib.cse_stft(None, None, 1, 100, 512, 128, None, None, None)
+    assert rc == -1
+    assert b"x is NULL" in lib.cse_last_error()
+    rc = lib.cse_stft(ctypes.c_void_p(16), None, 1, 100, 500, 128, None, None, None)
+    assert rc == -1 and b"n_fft" in lib.cse_last_error()
+    rc = lib.cse_enhance_cells(256, 100, ctypes.c_void_p(16), 1, ctypes.c_void_p(16),
+                               ctypes.c_void_p(16), None, None, None, None, None, None, None,
+                               None)
+    assert rc == -1 and b"n_fft" in lib.cse_last_error()
+    rc = lib.cse_noise_estimate(7, ctypes.c_void_p(16), 1, 100, 257, 20.0, 1e-10,
+                                ctypes.c_void_p(16), ctypes.c_void_p(16), None)
+    assert rc == -1 and b"Unbekannte Methode" in lib.cse_last_error()
+
+
+def test_cell_struct_layout():
+    assert _lib.CELL_DTYPE.itemsize == 88
+    off = {n: _lib.CELL_DTYPE.fields[n][1] for n in _lib.CELL_DTYPE.names}
+    assert off == {"algo": 0, "hop": 4, "y_offset": 8, "noise_offset": 16, "noise_stride": 24,
+                   "clean_offset": 32, "out_offset": 40, "gain_offset": 48, "param": 56}
+
+
+def test_workspace_size_is_positive(lib):
+    assert lib.cse_noise_workspace_bytes(4, 1251, 257) >= 4 * 1251 * 257 * 8
+
+
+def test_wave_packing_groups_and_pads():
+    from classical_speech_enhancement_amd.engine import pack_waves
+    cells = np.zeros(7, dtype=_lib.CELL_DTYPE)
+    cells["algo"] = [3, 3, 3, 3, 3, 0, 0]
+    cells["hop"] = [128, 128, 256, 128, 128, 128, 128]
+    cells["y_offset"] = [0, 0, 5, 0, 0, 0, 0]
+    packed, order = pack_waves(cells, 512)
+    assert len(packed) % 4 == 0
+    assert sorted(order[order >= 0].tolist()) == list(range(7))
+    for w in range(len(packed) // 4):
+        slots = packed[4 * w:4 * w + 4]
+        real = slots[slots["algo"] >= 0]
+        assert len(set(real["hop"].tolist())) == 1 and len(set(real["algo"].tolist())) == 1
+        assert slots[0]["algo"] >= 0
+    # longest first: hop 128 OMLSA before hop 128 SS and hop 256 OMLSA
+    assert packed[0]["algo"] == 3 and packed[0]["hop"] == 128
