@@ -60,7 +60,7 @@ def load(path=LIB_PATH):
     lib.cse_noise_estimate.restype = i32
     lib.cse_noise_estimate.argtypes = [i32, P, i64, i32, i32, f64, f64, P, P, P]
     lib.cse_noise_smooth.restype = i32
-    lib.cse_noise_smooth.argtypes = [P, i64, i32, i32, f64, f64, P, P]
+    lib.cse_noise_smooth.argtypes = [P, i64, i32, i32, i32, f64, P, P]
     lib.cse_istft_norm.restype = i32
     lib.cse_istft_norm.argtypes = [i32, i32, i64, P, P]
     lib.cse_enhance_cells.restype = i32

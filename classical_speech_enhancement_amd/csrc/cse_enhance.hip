@@ -198,8 +198,10 @@ __device__ __forceinline__ void gain_stage(const LaneCell& c, int i, int t, floa
         float g;
         cf Sj;
         if (ALGO == CSE_ALGO_SS) {
-            // spectral_subtractor.py:44-53: Ps = max(P - a N, b N); |S| = sqrt(Ps), phase of Y
-            const float n = fmaxf(nz, 1e-10f);
+            // spectral_subtractor.py:44-53: Ps = max(P - a N, b N); |S| = sqrt(Ps), phase of Y.
+            // No eps floor here: the reference floors BEFORE fix_length, so its
+            // zero-padded frames really subtract 0 (engine.noise_key).
+            const float n = nz;
             const float ps = fmaxf(P - c.p[0] * n, c.p[1] * n);
             const float sp = __builtin_amdgcn_sqrtf(ps);
             if (P > 0.0f) {

@@ -197,20 +197,18 @@ __global__ void floor_cast_kernel(const double* __restrict__ P, int64_t n, doubl
     if (i < n) N[i] = (float)fmax(P[i], eps);
 }
 
-__global__ void smooth_kernel(const float* __restrict__ N, int T, int B, double mu,
-                              double pre_eps, float* __restrict__ out) {
+__global__ void smooth_kernel(const float* __restrict__ N, int T, int B, int src_frames,
+                              double mu, float* __restrict__ out) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t sig = blockIdx.y;
     if (b >= B) return;
-    const float* Ns = N + sig * (int64_t)T * B + b;
+    const float* Ns = N + sig * (int64_t)src_frames * B + b;
     float* Os = out + sig * (int64_t)T * B + b;
     double s = (double)Ns[0];
-    if (pre_eps > 0.0) s = fmax(s, pre_eps);
     Os[0] = (float)s;
     const double c = 1.0 - mu;
     for (int t = 1; t < T; ++t) {
-        double n = (double)Ns[(int64_t)t * B];
-        if (pre_eps > 0.0) n = fmax(n, pre_eps);
+        const double n = t < src_frames ? (double)Ns[(int64_t)t * B] : 0.0;  // fix_length pad
         s = __dadd_rn(__dmul_rn(mu, s), __dmul_rn(c, n));
         Os[(int64_t)t * B] = (float)s;
     }
@@ -327,13 +325,15 @@ extern "C" int cse_noise_estimate(int method, const double* P, int64_t n_sig, in
     return CSE_OK;
 }
 
-extern "C" int cse_noise_smooth(const float* N, int64_t n_sig, int T, int B, double mu,
-                                double pre_eps, float* out, cse_stream_t stream) {
+extern "C" int cse_noise_smooth(const float* N, int64_t n_sig, int T, int B, int src_frames,
+                                double mu, float* out, cse_stream_t stream) {
     CSE_CHECK_ARG(N && out, "cse_noise_smooth: NULL pointer");
     CSE_CHECK_ARG(n_sig > 0 && n_sig < 65536 && T >= 1 && B >= 1, "cse_noise_smooth: bad shape");
+    CSE_CHECK_ARG(src_frames == 1 || src_frames == T, "cse_noise_smooth: src_frames=%d (1|T)",
+                  src_frames);
     const double m = fmin(fmax(mu, 0.0), 0.9999);
     hipLaunchKernelGGL(smooth_kernel, dim3(ceil_div(B, 64), (unsigned)n_sig), dim3(64), 0,
-                       (hipStream_t)stream, N, T, B, m, pre_eps, out);
+                       (hipStream_t)stream, N, T, B, src_frames, m, out);
     CSE_CHECK_LAUNCH("cse_noise_smooth");
     return CSE_OK;
 }

@@ -58,31 +58,46 @@ def n_frames(length, hop):
 def noise_key(alg, params, T):
     """Which noise PSD array a cell reads, mirroring each algorithm's pipeline.
 
-    Returns (kind, method, pct, eps, mu, pre_eps) where kind is 'static' or 'tv'.
+    Returns (method, pct, eps, expand, mu):
       - every algorithm estimates with the eps it passes (ss/wiener/omlsa 1e-10,
         mmse 1e-12: spectral_subtractor.py:17, wiener_filter.py:23, mmse.py:17,
         advanced_mmse.py:26);
-      - T < 5 -> the static simple estimate for ANY method
+      - T < 5 -> the static 'simple' estimate for ANY method
         (noise_estimation.py:194-195, before the method is even looked at);
-      - mmse/omlsa smooth time-varying estimates except true_noise
-        (mmse.py:48, advanced_mmse.py:60-66; omlsa floors at eps first, :51).
+      - expand: SS and OMLSA pass a static (B,1) estimate through
+        librosa.util.fix_length(..., size=T, axis=1) (spectral_subtractor.py:40-41,
+        advanced_mmse.py:54-55), which ZERO-PADS frames 1..T-1 — frame 0 sees
+        the estimate, later frames see 0 (SS) or, after OMLSA's smoothing,
+        mu**t times it;
+      - mmse/omlsa smooth any time-varying estimate except true_noise
+        (mmse.py:48-54, advanced_mmse.py:60-66); mu=None means no smoothing.
+    A key is static (one [B] row for all frames) iff expand is False and the
+    method is percentile/simple.
     """
     code, eps, _ = ALGOS[alg]
     method = params["noise_method"]
     if T < 5:
-        return ("static", "simple", None, eps, None, None)
-    if method == "percentile":
-        return ("static", "percentile", float(params["noise_percentile"]), eps, None, None)
-    if method == "min_tracking":
-        mu = pre = None
+        method, pct = "simple", None
+    elif method == "percentile":
+        pct = float(params["noise_percentile"])
+    elif method in ("min_tracking", "true_noise"):
+        pct = None
+    else:
+        raise ValueError(f"Unbekannte Methode: {method}")
+    static = method in ("percentile", "simple")
+    expand = static and T > 1 and code in ("SS", "OMLSA")
+    mu = None
+    if method != "true_noise" and (expand or not static):
         if code == "MMSE":
             mu = float(params.get("noise_mu", 0.98))
         elif code == "OMLSA":
-            mu, pre = float(params["noise_mu"]), eps
-        return ("tv", "min_tracking", None, eps, mu, pre)
-    if method == "true_noise":
-        return ("tv", "true_noise", None, eps, None, None)
-    raise ValueError(f"Unbekannte Methode: {method}")
+            mu = float(params["noise_mu"])
+    return (method, pct, eps, expand, mu)
+
+
+def key_is_static(key):
+    method, _, _, expand, mu = key
+    return method in ("percentile", "simple") and not expand and mu is None
 
 
 class Engine:
@@ -119,12 +134,14 @@ class Engine:
                    f"cse_noise_estimate({method})")
         return out
 
-    def noise_smooth(self, N, mu, pre_eps=None, out=None):
-        S, T, B = N.shape
-        out = torch.empty_like(N) if out is None else out
-        _lib.check(self.lib.cse_noise_smooth(_ptr(N), S, T, B, float(mu),
-                                             float(pre_eps or 0.0), _ptr(out), _stream()),
-                   "cse_noise_smooth")
+    def noise_smooth(self, N, T, mu, out=None):
+        """[S,T,B] (or static [S,B], zero-padded to T frames) -> smoothed [S,T,B]."""
+        S, B = N.shape[0], N.shape[-1]
+        src_frames = 1 if N.dim() == 2 else N.shape[1]
+        if out is None:
+            out = torch.empty((S, T, B), dtype=torch.float32, device=N.device)
+        _lib.check(self.lib.cse_noise_smooth(_ptr(N), S, T, B, src_frames, float(mu), _ptr(out),
+                                             _stream()), "cse_noise_smooth")
         return out
 
     def istft_norm(self, n_fft, hop, length):
@@ -196,7 +213,7 @@ class Engine:
         pool_parts, pool_off, noff = [], {}, 0
         true_P = {}
         for (hop, key) in keys:
-            kind, method, pct, eps, mu, pre = key
+            method, pct, eps, expand, mu = key
             T = n_frames(L, hop)
             P = P64[hop]
             if method == "true_noise":
@@ -209,8 +226,8 @@ class Engine:
                 N = self.noise_estimate("percentile", P, 25.0, eps)
             else:
                 N = self.noise_estimate(method, P, pct if pct is not None else 20.0, eps)
-            if mu is not None:
-                N = self.noise_smooth(N, mu, pre)
+            if expand or mu is not None:
+                N = self.noise_smooth(N, T, mu or 0.0)
             stride = 0 if N.dim() == 2 else B
             pool_parts.append(N.reshape(-1))
             pool_off[(hop, key)] = (noff, stride, N.shape[-1] if stride == 0 else T * B)

@@ -113,13 +113,16 @@ int cse_noise_estimate(int method, const double* P, int64_t n_sig, int T, int B,
                        cse_stream_t stream);
 
 /*
- * First-order IIR smoothing of a time-varying noise PSD over frames
- * (mmse.py:48-54, advanced_mmse.py:60-66): out_0 = N_0,
- * out_t = mu*out_{t-1} + (1-mu)*N_t with mu = clip(mu, 0, 0.9999), after an
- * optional floor N <- max(N, pre_eps) (pass pre_eps <= 0 for none).  fp64 math.
+ * Time-varying noise PSD for the smoothed / frame-padded cases, fp64 math:
+ *   src = N [n_sig][src_frames][B] with src_frames == T, or src_frames == 1: a
+ *   static estimate that librosa.util.fix_length(..., size=T, axis=1)
+ *   zero-pads to T frames (spectral_subtractor.py:40-41, advanced_mmse.py:54-55);
+ *   out_0 = src_0, out_t = mu*out_{t-1} + (1-mu)*src_t  (mmse.py:48-54,
+ *   advanced_mmse.py:60-66) with mu = clip(mu, 0, 0.9999); mu = 0 gives the
+ *   plain (padded) source.  out: [n_sig][T][B] f32.
  */
-int cse_noise_smooth(const float* N, int64_t n_sig, int T, int B, double mu,
-                     double pre_eps, float* out, cse_stream_t stream);
+int cse_noise_smooth(const float* N, int64_t n_sig, int T, int B, int src_frames, double mu,
+                     float* out, cse_stream_t stream);
 
 /*
  * 1 / window-sum-square of the ISTFT (librosa 0.11 istft normalisation) for a
