@@ -1,0 +1,239 @@
+#!/usr/bin/env python
+"""bench.py — STFT frame-gain evaluations/s on MI355X (BASELINE.json metric).
+
+Workload (one "step"): for P synthetic 10-s 16-kHz pairs per GPU, the n_fft=512
+half of the reference's full HEAD grid (parameter_ranges.py: SS 360 + MMSE 960
++ Wiener 96 + OMLSA 3456 = 4872 cells per pair, hops 128 and 256):
+  STFT + noise PSDs (percentile 10/20, min-tracking, smoothing)   [per pair]
+  fused gain recursion + ISTFT + clipped-SNR sums, every cell     [THE HOT PATH]
+  per-cell records (sse, finite) -> host, all-gathered over ranks [results table]
+Unit = one frame-gain evaluation = one cell x one STFT frame, all 257 bins
+(SURVEY §8(d)): 4,572,372 per pair.  Every cell is counted, including the
+quarter that are exact duplicates (min_tracking ignores noise_percentile).
+
+Multi-GPU: one process per GPU (torchrun), pairs sharded across ranks (weak
+scaling, no data-path collective); value = all ranks' units / max-rank time.
+
+    python bench.py [--gpus N --steps K --warmup W --pairs P]
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = ("STFT frame-gain evals/sec/node, 16kHz 512-pt FFT full grid; 1/2/4/8-GPU scaling")
+BYTES_PER_UNIT_512 = 12 * 257  # read P + read N + write G, fp32, per frame
+HBM_PEAK = 8.0e12              # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_PEAK = 157.3e12
+
+
+from classical_speech_enhancement_amd.parameter_ranges import grid_specs  # noqa: E402
+
+
+def _cpu_cell(args):
+    alg, params, seconds = args
+    import oracle
+    from classical_speech_enhancement_amd.synth import make_pair
+    clean, noisy = _cpu_cell.pair if hasattr(_cpu_cell, "pair") else (None, None)
+    if clean is None:
+        clean, noisy = make_pair(0, seconds)
+        _cpu_cell.pair = (clean, noisy)
+    kw = dict(params)
+    if kw["noise_method"] == "true_noise":
+        kw["clean_audio"] = clean
+    fn = oracle.ALGORITHMS[alg]
+    y = fn(noisy, 16000, **kw)
+    e = np.clip(y, -1, 1)
+    oracle.calculate_snr(clean, e)
+    return 1 + int(len(noisy)) // int(params["hop_length"])
+
+
+def cpu_baseline(budget_s=15.0, seconds=10.0, n_fft=512):
+    """The oracle (the reference's algorithm restated, fp64, per-frame Python
+    loops, one STFT+estimate per cell exactly like the reference) on the host
+    cores, over cells drawn uniformly at random from the same grid, for a fixed
+    wall-clock budget.  Returns frame-gain evals/s."""
+    import multiprocessing as mp
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(16, cores))
+    specs = grid_specs(1, n_fft)
+    rng = np.random.default_rng(0)
+    order = rng.permutation(len(specs))
+    work = [(specs[i][1], specs[i][2], seconds) for i in order]
+    env_keys = ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")
+    saved = {k: os.environ.get(k) for k in env_keys}
+    for k in env_keys:
+        os.environ[k] = "1"
+    ctx = mp.get_context("spawn")
+    units = cells = 0
+    try:
+        with ctx.Pool(cores) as pool:
+            # warm the workers (imports + synth) outside the window
+            list(pool.imap_unordered(_cpu_cell, work[:cores]))
+            t0 = time.perf_counter()
+            it = pool.imap_unordered(_cpu_cell, work[cores:] * 4, chunksize=1)
+            for u in it:
+                units += u
+                cells += 1
+                if time.perf_counter() - t0 > budget_s:
+                    break
+            dt = time.perf_counter() - t0
+            pool.terminate()
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return {"value": units / dt, "unit": "frame-gain evals/s", "cores": cores, "kind": "port",
+            "sample": (f"{cells} cells drawn uniformly from the n_fft={n_fft} HEAD grid, "
+                       f"one 10-s pair, oracle/ fp64 numpy (reference algorithm incl. per-cell "
+                       f"STFT+noise estimate), {cores} single-threaded processes, "
+                       f"{dt:.1f} s wall")}
+
+
+def load_traffic(units_per_launch):
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        if d.get("units_per_launch") == units_per_launch:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs", type=int, default=8, help="10-s pairs per GPU")
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    from classical_speech_enhancement_amd.engine import Engine, snr_db
+    from classical_speech_enhancement_amd.synth import make_pair
+
+    eng = Engine()
+    P = args.pairs
+    pairs = [make_pair(rank * P + i, args.seconds) for i in range(P)]
+    clean = torch.as_tensor(np.stack([c for c, _ in pairs])).cuda()
+    noisy = torch.as_tensor(np.stack([n for _, n in pairs])).cuda()
+    clean_pow = (clean ** 2).sum(dim=1).cpu().numpy()
+    L = noisy.shape[1]
+    specs = grid_specs(P, 512)
+    mp = eng.plan(P, L, specs, with_clean=True)
+    plan = mp.plans[0]
+    units = mp.units
+
+    def step(ev=None):
+        plan.prepare(noisy, clean)
+        if ev is not None:
+            ev[0].record()
+        plan.enhance()
+        if ev is not None:
+            ev[1].record()
+        rec = torch.stack([plan.sse_d, plan.fin_d.double()])
+        if world > 1:
+            out = torch.empty((world,) + rec.shape, dtype=rec.dtype, device=rec.device)
+            dist.all_gather_into_tensor(out, rec)
+            rec = out
+        return rec.cpu()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        rec = step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+
+    # sanity of the step's output: every cell finite, SNRs finite
+    sse, fin = plan.results()[:2]
+    assert fin.all(), "non-finite enhanced output"
+    snr = snr_db(sse, clean_pow[[s for (s, _, _) in specs]])
+    assert np.isfinite(snr).all()
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    total_units = units * world * args.steps
+    value = total_units / dt
+    achieved = units * BYTES_PER_UNIT_512 / (kern_ms / 1e3)
+    traffic = load_traffic(units)
+    res = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "frame-gain evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": (f"{P} x 10-s 16-kHz synthetic pairs per GPU, HEAD parameter_ranges.py "
+                         f"grid at n_fft=512 (all 4 algorithms, 4872 cells/pair, hops 128+256): "
+                         f"STFT+noise PSDs+fused gain/ISTFT/SNR per cell"),
+            "pairs_per_gpu": P, "clip_s": args.seconds, "sr": 16000, "n_fft": 512,
+            "cells_per_gpu": len(specs), "units_per_step_per_gpu": units,
+            "parallelism": f"pairs sharded over {world} rank(s), all_gather of per-cell records",
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK, "traffic": traffic,
+            "kernel": "cse::enhance_kernel<512>", "kernel_ms": kern_ms,
+            "bytes_per_unit": BYTES_PER_UNIT_512, "units_per_launch": units,
+        },
+    }
+    if not args.no_cpu_baseline and world == 1:
+        res["cpu_baseline"] = cpu_baseline(args.cpu_budget, args.seconds)
+    print(json.dumps(res))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

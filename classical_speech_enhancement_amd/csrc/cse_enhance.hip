@@ -45,7 +45,7 @@ struct Args {
     int64_t n_cells;
     const float2* Y;
     const float* noise;
-    const float* clean;
+    const double* clean;
     const float* inv_wss128;
     const float* inv_wss256;
     float* y_out;
@@ -174,7 +174,7 @@ struct LaneCell {
     const float2* Y;
     const float* N;
     int64_t nstride;
-    const float* clean;
+    const double* clean;
     float* out;
     float* gout;
     float p[8];
@@ -358,7 +358,7 @@ __device__ void run_cells(const Args& a, const LaneCell& c, int algo, cf* lds, c
                 if (c.out) c.out[o] = y;
                 if (c.clean) {
                     const float yc = fminf(fmaxf(y, -1.0f), 1.0f);
-                    const double d = (double)c.clean[o] - (double)yc;
+                    const double d = c.clean[o] - (double)yc;
                     sse = fma(d, d, sse);
                 }
             }
@@ -428,7 +428,7 @@ __global__ void __launch_bounds__(64) enhance_kernel(Args a) {
 using namespace cse;
 
 extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
-                                 const float* Y, const float* noise, const float* clean,
+                                 const float* Y, const float* noise, const double* clean,
                                  const float* inv_wss128, const float* inv_wss256, float* y_out,
                                  float* g_out, double* sse, uint8_t* finite,
                                  cse_stream_t stream) {

@@ -151,22 +151,186 @@ class Engine:
         return out
 
     # ------------------------------------------------------------------ grid
+    def plan(self, n_signals, length, specs, with_clean=True, want_waveforms=False,
+             want_gains=False):
+        """Build one GridPlan per n_fft for these specs (see GridPlan)."""
+        return MultiPlan(self, n_signals, length, specs, with_clean, want_waveforms, want_gains)
+
     def run(self, noisy, specs, clean=None, want_waveforms=False, want_gains=False):
         """Enhance every cell spec; returns a dict of per-spec results.
 
         noisy/clean: [S, L] float64 cuda tensors (clean may be None if no spec
         uses true_noise and no SNR is wanted).  specs: list of
-        (signal_index, algorithm_name, params).  Results (numpy, spec order):
-          sse [n] f64, finite [n] bool, and optionally 'y' [n, L] f32 (cuda)
-          and 'G' list of [T, B] f32 (cuda).
+        (signal_index, algorithm_name, params).  Results (spec order):
+          sse [n] f64 numpy, finite [n] bool numpy, and optionally
+          'y' [n, L] f32 cuda and 'G' list of [T, B] f32 cuda.
         """
         S, L = noisy.shape
-        n = len(specs)
-        sse = np.full(n, np.nan)
-        finite = np.zeros(n, dtype=bool)
-        y_all = (torch.zeros((n, L), dtype=torch.float32, device=noisy.device)
-                 if want_waveforms else None)
-        gains = [None] * n if want_gains else None
+        mp = self.plan(S, L, specs, clean is not None, want_waveforms, want_gains)
+        mp.execute(noisy, clean)
+        return mp.results()
+
+
+class GridPlan:
+    """Everything one n_fft's cells need, allocated once; execute() only enqueues.
+
+    Buffers (device, resident in HBM across steps):
+      Y      [hop][S][T][B] complex64        cse_stft
+      P      [S][T][B] f64 per hop           cse_stft (analysis power)
+      pool   flat f32: every noise PSD the cells read, at per-key offsets
+      cells  packed cse_cell_t table (wave slots, longest-first)
+      sse/finite per packed cell; optional y_out / g_out
+    execute() issues only kernel launches on the current stream (no host
+    sync, no allocation), so it can be timed or captured as a graph.
+    """
+
+    def __init__(self, eng, n_fft, S, L, items, with_clean, want_y, want_g, y_all=None):
+        self.eng, self.n_fft, self.S, self.L = eng, n_fft, S, L
+        self.items = items
+        dev = eng.device
+        B = self.B = n_fft // 2 + 1
+        self.hops = sorted({p["hop_length"] for (_, _, _, p) in items})
+        self.y_base, off = {}, 0
+        for hop in self.hops:
+            self.y_base[hop] = off
+            off += S * n_frames(L, hop) * B
+        self.Ybuf = torch.empty(off * 2, dtype=torch.float32, device=dev)
+        self.P = {h: torch.empty((S, n_frames(L, h), B), dtype=torch.float64, device=dev)
+                  for h in self.hops}
+        self.Ptrue = {}
+        # ---- noise keys -> pool slices
+        keys = {}
+        for (_, _, alg, p) in items:
+            T = n_frames(L, p["hop_length"])
+            keys.setdefault((p["hop_length"], noise_key(alg, p, T)), None)
+        self.keys = list(keys)
+        self.pool_off, noff, tmp_need = {}, 0, 0
+        for (hop, key) in self.keys:
+            T = n_frames(L, hop)
+            static = key_is_static(key)
+            per_sig = B if static else T * B
+            self.pool_off[(hop, key)] = (noff, 0 if static else B, per_sig)
+            noff += S * per_sig
+            method, _, _, expand, mu = key
+            if method == "true_noise" and hop not in self.Ptrue:
+                if not with_clean:
+                    raise ValueError("TrueNoiseEstimator requires clean_audio and noisy_audio")
+                self.Ptrue[hop] = torch.empty((S, T, B), dtype=torch.float64, device=dev)
+            if expand or mu is not None:  # estimate into scratch, then smooth into the pool
+                tmp_need = max(tmp_need, S * T * B)
+        self.pool = torch.empty(noff, dtype=torch.float32, device=dev)
+        self.scratch = torch.empty(max(tmp_need, 1), dtype=torch.float32, device=dev)
+        Tmax = max(n_frames(L, h) for h in self.hops)
+        self.ws = torch.empty(int(eng.lib.cse_noise_workspace_bytes(S, Tmax, B)),
+                              dtype=torch.uint8, device=dev)
+        self.inv = {h: eng.istft_norm(n_fft, h, L) for h in self.hops}
+        # ---- cell table
+        cells = np.zeros(len(items), dtype=_lib.CELL_DTYPE)
+        g_total = 0
+        self.g_offsets = []
+        for c, (idx, sig, alg, p) in enumerate(items):
+            code, _, names = ALGOS[alg]
+            hop = p["hop_length"]
+            T = n_frames(L, hop)
+            o, stride, per_sig = self.pool_off[(hop, noise_key(alg, p, T))]
+            cells["algo"][c] = _lib.ALGO[code]
+            cells["hop"][c] = hop
+            cells["y_offset"][c] = self.y_base[hop] + sig * T * B
+            cells["noise_offset"][c] = o + sig * per_sig
+            cells["noise_stride"][c] = stride
+            cells["clean_offset"][c] = sig * L if with_clean else -1
+            cells["out_offset"][c] = idx * L if want_y else -1
+            cells["gain_offset"][c] = g_total if want_g else -1
+            self.g_offsets.append((g_total, T))
+            if want_g:
+                g_total += T * B
+            prm = [float(p[k]) for k in names]
+            cells["param"][c, :len(prm)] = prm
+        self.cells = cells
+        packed, self.order = pack_waves(cells, n_fft)
+        self.n_packed = len(packed)
+        self.cells_d = torch.from_numpy(packed.view(np.uint8).copy()).to(dev)
+        self.g_out = torch.zeros(max(g_total, 1), dtype=torch.float32, device=dev) if want_g else None
+        self.y_all = y_all
+        self.sse_d = torch.zeros(self.n_packed, dtype=torch.float64, device=dev)
+        self.fin_d = torch.zeros(self.n_packed, dtype=torch.uint8, device=dev)
+        self.clean = None
+        self.with_clean = with_clean
+        # frame-gain evaluations (SURVEY §8(d) unit): sum over cells of frames
+        self.units = int(sum(n_frames(L, p["hop_length"]) for (_, _, _, p) in items))
+
+    def _est(self, method, P, pct, eps, out):
+        S, T, B = P.shape
+        code = {"percentile": 0, "min_tracking": 1, "true_noise": 2}[method]
+        _lib.check(self.eng.lib.cse_noise_estimate(code, _ptr(P), S, T, B, float(pct), float(eps),
+                                                   _ptr(out), _ptr(self.ws), _stream()),
+                   f"cse_noise_estimate({method})")
+
+    def prepare(self, noisy, clean=None):
+        """Group-level analysis: STFTs, noise PSDs (once per signal batch)."""
+        eng, S, L, B = self.eng, self.S, self.L, self.B
+        lib = eng.lib
+        for hop in self.hops:
+            T = n_frames(L, hop)
+            yv = self.Ybuf[2 * self.y_base[hop]:2 * (self.y_base[hop] + S * T * B)]
+            _lib.check(lib.cse_stft(_ptr(noisy), None, S, L, self.n_fft, hop, _ptr(yv),
+                                    _ptr(self.P[hop]), _stream()), "cse_stft")
+            if hop in self.Ptrue:
+                _lib.check(lib.cse_stft(_ptr(noisy), _ptr(clean), S, L, self.n_fft, hop, None,
+                                        _ptr(self.Ptrue[hop]), _stream()), "cse_stft(true)")
+        for (hop, key) in self.keys:
+            method, pct, eps, expand, mu = key
+            T = n_frames(L, hop)
+            o, stride, per_sig = self.pool_off[(hop, key)]
+            dst = self.pool[o:o + S * per_sig]
+            smooth = expand or mu is not None
+            tgt = self.scratch if smooth else dst
+            if method == "true_noise":
+                self._est("true_noise", self.Ptrue[hop], 0.0, eps, tgt)
+            elif method == "simple":
+                self._est("percentile", self.P[hop], 25.0, eps, tgt)
+            else:
+                self._est(method, self.P[hop], pct if pct is not None else 20.0, eps, tgt)
+            if smooth:
+                src_frames = 1 if method in ("percentile", "simple") else T
+                _lib.check(lib.cse_noise_smooth(_ptr(tgt), S, T, B, src_frames, float(mu or 0.0),
+                                                _ptr(dst), _stream()), "cse_noise_smooth")
+        self.clean = clean if self.with_clean else None
+
+    def enhance(self):
+        """THE HOT PATH launch: every cell of this n_fft, one kernel."""
+        _lib.check(self.eng.lib.cse_enhance_cells(
+            self.n_fft, self.L, _ptr(self.cells_d), self.n_packed, _ptr(self.Ybuf),
+            _ptr(self.pool), _ptr(self.clean), _ptr(self.inv.get(128)), _ptr(self.inv.get(256)),
+            _ptr(self.y_all), _ptr(self.g_out), _ptr(self.sse_d), _ptr(self.fin_d), _stream()),
+            "cse_enhance_cells")
+
+    def execute(self, noisy, clean=None):
+        self.prepare(noisy, clean)
+        self.enhance()
+
+    def results(self):
+        sse_p = self.sse_d.cpu().numpy()
+        fin_p = self.fin_d.cpu().numpy().astype(bool)
+        real = self.order >= 0
+        sse = np.empty(len(self.items))
+        fin = np.empty(len(self.items), dtype=bool)
+        sse[self.order[real]] = sse_p[real]
+        fin[self.order[real]] = fin_p[real]
+        G = None
+        if self.g_out is not None:
+            G = [self.g_out[g0:g0 + T * self.B].view(T, self.B) for (g0, T) in self.g_offsets]
+        return sse, fin, G
+
+
+class MultiPlan:
+    """GridPlans for every n_fft present in a spec list (spec order preserved)."""
+
+    def __init__(self, eng, S, L, specs, with_clean, want_y, want_g):
+        self.n = len(specs)
+        self.want_g = want_g
+        self.y_all = (torch.zeros((self.n, L), dtype=torch.float32, device=eng.device)
+                      if want_y else None)
         by_fft = {}
         for idx, (sig, alg, params) in enumerate(specs):
             alg = canonical_algo(alg)
@@ -174,112 +338,37 @@ class Engine:
             p.update(params)
             if p["hop_length"] not in (128, 256) or p["n_fft"] not in (512, 1024):
                 raise ValueError("engine supports n_fft in {512,1024}, hop in {128,256}")
-            if p["noise_method"] == "true_noise" and clean is None and n_frames(L, p["hop_length"]) >= 5:
+            if not 0 <= int(sig) < S:
+                raise ValueError(f"signal index {sig} out of range")
+            noise_key(alg, p, n_frames(L, p["hop_length"]))  # validates the method
+            if (p["noise_method"] == "true_noise" and not with_clean
+                    and n_frames(L, p["hop_length"]) >= 5):
                 raise ValueError("TrueNoiseEstimator requires clean_audio and noisy_audio")
             by_fft.setdefault(int(p["n_fft"]), []).append((idx, int(sig), alg, p))
-        for n_fft, items in by_fft.items():
-            res = self._run_fft(n_fft, noisy, clean, items, want_waveforms, want_gains, y_all)
-            for (idx, *_), s, f, g in zip(items, res["sse"], res["finite"], res["G"]):
-                sse[idx], finite[idx] = s, f
-                if want_gains:
-                    gains[idx] = g
-        out = {"sse": sse, "finite": finite}
-        if want_waveforms:
-            out["y"] = y_all
-        if want_gains:
+        self.plans = [GridPlan(eng, n_fft, S, L, items, with_clean, want_y, want_g, self.y_all)
+                      for n_fft, items in sorted(by_fft.items())]
+        self.units = sum(p.units for p in self.plans)
+
+    def execute(self, noisy, clean=None):
+        for p in self.plans:
+            p.execute(noisy, clean)
+
+    def results(self):
+        sse = np.full(self.n, np.nan)
+        fin = np.zeros(self.n, dtype=bool)
+        gains = [None] * self.n if self.want_g else None
+        for p in self.plans:
+            s, f, G = p.results()
+            for c, (idx, *_rest) in enumerate(p.items):
+                sse[idx], fin[idx] = s[c], f[c]
+                if gains is not None:
+                    gains[idx] = G[c]
+        out = {"sse": sse, "finite": fin}
+        if self.y_all is not None:
+            out["y"] = self.y_all
+        if gains is not None:
             out["G"] = gains
         return out
-
-    def _run_fft(self, n_fft, noisy, clean, items, want_y, want_g, y_all):
-        S, L = noisy.shape
-        B = n_fft // 2 + 1
-        hops = sorted({p["hop_length"] for (_, _, _, p) in items})
-        # ---- spectra of every signal at every hop, one buffer (y_offset per cell)
-        y_base, y_parts, P64 = {}, [], {}
-        off = 0
-        for hop in hops:
-            T = n_frames(L, hop)
-            Y, P = self.stft(noisy, n_fft, hop)
-            y_parts.append(Y.reshape(-1))
-            y_base[hop] = off
-            off += S * T * B
-            P64[hop] = P
-        Ybuf = torch.cat(y_parts) if len(y_parts) > 1 else y_parts[0]
-        # ---- noise pool: every distinct PSD the cells read
-        keys = {}
-        for (_, _, alg, p) in items:
-            T = n_frames(L, p["hop_length"])
-            keys.setdefault((p["hop_length"], noise_key(alg, p, T)), None)
-        pool_parts, pool_off, noff = [], {}, 0
-        true_P = {}
-        for (hop, key) in keys:
-            method, pct, eps, expand, mu = key
-            T = n_frames(L, hop)
-            P = P64[hop]
-            if method == "true_noise":
-                if hop not in true_P:
-                    if clean is None:
-                        raise ValueError("TrueNoiseEstimator requires clean_audio and noisy_audio")
-                    true_P[hop] = self.stft(noisy, n_fft, hop, x_sub=clean, want_y=False)[1]
-                N = self.noise_estimate("true_noise", true_P[hop], eps=eps)
-            elif method == "simple":
-                N = self.noise_estimate("percentile", P, 25.0, eps)
-            else:
-                N = self.noise_estimate(method, P, pct if pct is not None else 20.0, eps)
-            if expand or mu is not None:
-                N = self.noise_smooth(N, T, mu or 0.0)
-            stride = 0 if N.dim() == 2 else B
-            pool_parts.append(N.reshape(-1))
-            pool_off[(hop, key)] = (noff, stride, N.shape[-1] if stride == 0 else T * B)
-            noff += N.numel()
-        pool = torch.cat(pool_parts) if len(pool_parts) > 1 else pool_parts[0]
-        inv = {h: self.istft_norm(n_fft, h, L) for h in hops}
-        # ---- cells
-        G_bufs = [None] * len(items)
-        cells = np.zeros(len(items), dtype=_lib.CELL_DTYPE)
-        g_total = 0
-        for c, (idx, sig, alg, p) in enumerate(items):
-            code, _, names = ALGOS[alg]
-            hop = p["hop_length"]
-            T = n_frames(L, hop)
-            o, stride, per_sig = pool_off[(hop, noise_key(alg, p, T))]
-            cells["algo"][c] = _lib.ALGO[code]
-            cells["hop"][c] = hop
-            cells["y_offset"][c] = y_base[hop] + sig * T * B
-            cells["noise_offset"][c] = o + sig * per_sig
-            cells["noise_stride"][c] = stride
-            cells["clean_offset"][c] = sig * L if clean is not None else -1
-            cells["out_offset"][c] = idx * L if want_y else -1
-            if want_g:
-                cells["gain_offset"][c] = g_total
-                g_total += T * B
-            else:
-                cells["gain_offset"][c] = -1
-            prm = [float(p[k]) for k in names]
-            cells["param"][c, :len(prm)] = prm
-        packed, order = pack_waves(cells, n_fft)
-        dev = noisy.device
-        cells_d = torch.from_numpy(packed.view(np.uint8)).to(dev)
-        g_out = torch.zeros(g_total, dtype=torch.float32, device=dev) if want_g else None
-        sse_d = torch.zeros(len(packed), dtype=torch.float64, device=dev)
-        fin_d = torch.zeros(len(packed), dtype=torch.uint8, device=dev)
-        clean32 = clean.to(torch.float32).contiguous() if clean is not None else None
-        _lib.check(self.lib.cse_enhance_cells(
-            n_fft, L, _ptr(cells_d), len(packed), _ptr(Ybuf), _ptr(pool), _ptr(clean32),
-            _ptr(inv.get(128)), _ptr(inv.get(256)), _ptr(y_all), _ptr(g_out), _ptr(sse_d),
-            _ptr(fin_d), _stream()), "cse_enhance_cells")
-        sse_p = sse_d.cpu().numpy()
-        fin_p = fin_d.cpu().numpy().astype(bool)
-        sse = np.empty(len(items))
-        fin = np.empty(len(items), dtype=bool)
-        sse[order[order >= 0]] = sse_p[order >= 0]
-        fin[order[order >= 0]] = fin_p[order >= 0]
-        if want_g:
-            for c, (idx, sig, alg, p) in enumerate(items):
-                T = n_frames(L, p["hop_length"])
-                g0 = int(cells["gain_offset"][c])
-                G_bufs[c] = g_out[g0:g0 + T * B].view(T, B)
-        return {"sse": sse, "finite": fin, "G": G_bufs}
 
 
 def pack_waves(cells, n_fft):

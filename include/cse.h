@@ -137,7 +137,8 @@ int cse_istft_norm(int n_fft, int hop, int64_t len, float* out, cse_stream_t str
  * phase), inverse real FFT, periodic-Hann synthesis window, overlap-add,
  * window-sum-square normalisation (librosa istft, length = len), and the
  * per-cell score reductions:
- *   sse[c]    = sum_n (clean[n] - clip(y[n], -1, 1))^2   (f64; if clean_offset >= 0)
+ *   sse[c]    = sum_n (clean[n] - clip(y[n], -1, 1))^2   (f64; clean is f64 [..][len],
+ *               used if clean_offset >= 0)
  *   finite[c] = 1 if every y[n] is finite
  * Optional outputs: y_out (the enhanced waveform, f32, [len] at out_offset)
  * and g_out (the gain matrix, f32 [T][B] at gain_offset).
@@ -146,7 +147,7 @@ int cse_istft_norm(int n_fft, int hop, int64_t len, float* out, cse_stream_t str
  * n_fft in {512, 1024}; hop in {128, 256}.
  */
 int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
-                      const float* Y, const float* noise, const float* clean,
+                      const float* Y, const float* noise, const double* clean,
                       const float* inv_wss128, const float* inv_wss256,
                       float* y_out, float* g_out, double* sse, uint8_t* finite,
                       cse_stream_t stream);
