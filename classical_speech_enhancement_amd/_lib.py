@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcse.so")
+LIB_PATH = os.environ.get("CSE_LIB", os.path.join(HERE, "libcse.so"))
 
 CSE_OK = 0
 ALGO = {"NONE": -1, "SS": 0, "WIENER": 1, "MMSE": 2, "OMLSA": 3}
@@ -28,8 +28,9 @@ EXPORTS = ("cse_version", "cse_last_error", "cse_stft", "cse_noise_workspace_byt
            "cse_noise_estimate", "cse_noise_smooth", "cse_istft_norm", "cse_enhance_cells")
 
 
-def cells_per_wave(n_fft):
-    return 4 if n_fft == 512 else 2
+def cells_per_group(n_fft):
+    """Cells per 256-thread workgroup slot group (CSE_CELLS_PER_GROUP)."""
+    return 16 if n_fft == 512 else 8
 
 
 class CseError(RuntimeError):
@@ -64,7 +65,7 @@ def load(path=LIB_PATH):
     lib.cse_istft_norm.restype = i32
     lib.cse_istft_norm.argtypes = [i32, i32, i64, P, P]
     lib.cse_enhance_cells.restype = i32
-    lib.cse_enhance_cells.argtypes = [i32, i64, P, i64, P, P, P, P, P, P, P, P, P, P]
+    lib.cse_enhance_cells.argtypes = [i32, i64, P, i64, P, P, P, P, P, P, P, P]
     _lib = lib
     return lib
 

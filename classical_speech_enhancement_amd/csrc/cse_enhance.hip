@@ -46,8 +46,6 @@ struct Args {
     const float2* Y;
     const float* noise;
     const double* clean;
-    const float* inv_wss128;
-    const float* inv_wss256;
     float* y_out;
     float* g_out;
     double* sse;
@@ -168,109 +166,169 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-struct LaneCell {
-    bool valid;
-    int algo;
-    const float2* Y;
-    const float* N;
-    int64_t nstride;
-    const double* clean;
-    float* out;
-    float* gout;
-    float p[8];
+// ---------------------------------------------------------------------------
+// Workgroup = 4 waves = CPWG cells that share hop, algorithm, spectrum Y,
+// noise PSD and clean reference (the host packs them so).  Per frame the
+// workgroup stages the shared rows (Y[t][:], N[t][:], clean[retired samples])
+// into LDS once, cooperatively, one frame ahead (a few VGPRs per thread),
+// instead of every lane keeping 17 bins of loads in flight.
+// ---------------------------------------------------------------------------
+template <int NFFT>
+struct WG {
+    using G = Geo<NFFT>;
+    static constexpr int WAVES = 4;
+    static constexpr int THREADS = 64 * WAVES;
+    static constexpr int CPWG = WAVES * G::CPW;                  // cells per workgroup
+    static constexpr int HMAX = 256;                              // largest hop
+    // per-cell LDS region: S row (B complex) aliased with the 16 x L transpose;
+    // stride = 64 B mod 256 B so the cells sharing a 32-lane group use
+    // disjoint bank halves in the transposed read.
+    static constexpr int CREG = ((G::B * 8 - 64 + 255) / 256) * 256 + 64;   // bytes
+    static constexpr int OFF_CELLS = 0;
+    static constexpr int OFF_Y = CPWG * CREG;                     // float2[B]
+    static constexpr int OFF_N = OFF_Y + ((G::B * 8 + 15) / 16) * 16;   // float[B]
+    static constexpr int OFF_C = OFF_N + ((G::B * 4 + 15) / 16) * 16;   // float[2][HMAX]
+    static constexpr int OFF_TW = OFF_C + 2 * HMAX * 4;           // cf[15][L] (b = 1..15)
+    static constexpr int BYTES = OFF_TW + 15 * G::L * 8;
+    static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
 };
 
-// gain stage of one frame: S[j] = Y[k_j] * G(k_j) for the lane's 16 (+1) bins
-template <int ALGO, int NFFT>
-__device__ __forceinline__ void gain_stage(const LaneCell& c, int i, int t, float (&rr)[17],
-                                           float lg2_floor, float q_spp, cf* sb) {
-    using G = Geo<NFFT>;
-    constexpr int M = G::M, L = G::L, B = G::B;
-    const float2* Yt = c.Y + (int64_t)t * B;
-    const float* Nt = c.N + (int64_t)t * c.nstride;
-    const bool first = (t == 0);
-#pragma unroll
-    for (int j = 0; j < 17; ++j) {
-        const int k = (j < 16) ? i + L * j : M;
-        const float2 y = c.valid ? Yt[k] : make_float2(0.f, 0.f);
-        const float nz = c.valid ? Nt[k] : 1.0f;
-        const float P = y.x * y.x + y.y * y.y;
-        float g;
-        cf Sj;
-        if (ALGO == CSE_ALGO_SS) {
-            // spectral_subtractor.py:44-53: Ps = max(P - a N, b N); |S| = sqrt(Ps), phase of Y.
-            // No eps floor here: the reference floors BEFORE fix_length, so its
-            // zero-padded frames really subtract 0 (engine.noise_key).
-            const float n = nz;
-            const float ps = fmaxf(P - c.p[0] * n, c.p[1] * n);
-            const float sp = __builtin_amdgcn_sqrtf(ps);
-            if (P > 0.0f) {
-                g = sp * __builtin_amdgcn_rsqf(P);
-                Sj = cmk(y.x * g, y.y * g);
-            } else {  // angle(0) = 0
-                g = 0.0f;
-                Sj = cmk(sp, 0.0f);
-            }
-        } else {
-            if (ALGO == CSE_ALGO_WIENER)
-                g = gain_wiener(P, nz, first, rr[j], c.p[0], c.p[1]);
-            else if (ALGO == CSE_ALGO_MMSE)
-                g = gain_mmse(P, nz, first, rr[j], c.p[0], c.p[1], c.p[2], c.p[3]);
-            else
-                g = gain_omlsa(P, nz, first, rr[j], c.p[0], c.p[1], c.p[2], lg2_floor, q_spp,
-                               c.p[4]);
-            Sj = cmk(y.x * g, y.y * g);
-        }
-        if (j < 16 || i == 0) {
-            sb[k] = Sj;
-            if (c.gout) c.gout[(int64_t)t * B + k] = g;
-        }
-    }
+// transposed-block column swizzle (bank-conflict-free reads, see WG::CREG)
+static_assert(WG<512>::BYTES <= 163840 / 4, "n_fft=512 workgroup must fit 4 per CU");
+
+// waves per SIMD the register allocation targets (VGPR budget 512 / w)
+#ifndef CSE_WAVES_PER_SIMD
+#define CSE_WAVES_PER_SIMD 2
+#endif
+
+template <int L>
+__device__ __forceinline__ int tswz(int b) { return L == 16 ? (b >> 1) : b; }
+
+// The (fp64-exact) window-sum-square of librosa istft at padded position p is
+// sum_r w^2(n + r*HOP) over the frames that cover p.  With all R frames present
+// it is 1.5 (R=4) / 3 (R=8) for the periodic Hann, or 0.75 + 0.25 cos(2π n/256)
+// for 512/256 (R=2); the first R-1 and the flush frames take the exact sum.
+template <int NFFT>
+__device__ __forceinline__ float hann_at(int aidx, int e, const float (&wc)[2],
+                                         const float (&ws)[2]) {
+    // w(n)/NFFT at n = SP*aidx + off + e (wc/ws carry the lane phase, pre-scaled)
+    const float ca = Rot32::c[(2 * aidx) & 31], sa = Rot32::s[(2 * aidx) & 31];
+    return 0.5f / NFFT - (ca * wc[e] - sa * ws[e]);
 }
 
-template <int NFFT, int HOP>
-__device__ void run_cells(const Args& a, const LaneCell& c, int algo, cf* lds, const cf* tw1,
-                          int64_t cell_idx) {
+template <int NFFT, int HOP, int ALGO, bool OUT>
+__device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, int n_cells_wg,
+                                       unsigned char* smem) {
     using G = Geo<NFFT>;
+    using W = WG<NFFT>;
     constexpr int M = G::M, L = G::L, B = G::B, SP = G::SP;
     constexpr int R = NFFT / HOP;       // frames overlapping one sample
     constexpr int F = 2 * HOP / SP;     // samples a lane retires per frame
     static_assert(F >= 2 && F <= 32 && (F % 2) == 0, "hop/n_fft combination");
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
     const int cs = lane / L, i = lane % L;
-    cf* sb = lds + cs * G::SROW;
-    cf* tb = lds + cs * G::TCELL;
-    const int64_t len = a.len;
+    const int cslot = wave * G::CPW + cs;
+    cf* sb = (cf*)(smem + W::OFF_CELLS + cslot * W::CREG);
+    cf* tb = sb;  // aliased: S row until pass 1 is done, then the transpose block
+    float2* yrow = (float2*)(smem + W::OFF_Y);
+    float* nrow = (float*)(smem + W::OFF_N);
+    float* crow = (float*)(smem + W::OFF_C);
+    const cf* tw1 = (const cf*)(smem + W::OFF_TW);
+
+    // ---- the shared rows of this workgroup (first cell's; host-validated)
+    const int len = (int)a.len;
+    const float2* Ybase = a.Y + wcell[0].y_offset;
+    const float* Nbase = a.noise + wcell[0].noise_offset;
+    const int64_t nstride = wcell[0].noise_stride;
+    const double* cbase = (a.clean && wcell[0].clean_offset >= 0) ? a.clean + wcell[0].clean_offset
+                                                                  : nullptr;
+    // without a clean reference the sums are of y^2 (crow rows stay 0)
     const int T = 1 + (int)(len / HOP);
     const int need = (int)((len + NFFT + HOP - 1) / HOP);
     const int nf = need < T ? need : T;
-    const float* invw = (HOP == 128) ? a.inv_wss128 : a.inv_wss256;
 
-    // lane-constant rotors: e^{2πi i/NFFT} (real-IFFT packing) and the window phase
-    float bs, bc;
+    // ---- my cell
+    const bool valid = cslot < n_cells_wg && wcell[cslot].algo == ALGO;
+    const cse_cell_t* cp = wcell + (cslot < n_cells_wg ? cslot : 0);
+    float p0 = cp->param[0], p1 = cp->param[1], p2 = cp->param[2], p3 = cp->param[3],
+          p4 = cp->param[4];
+    float* yout = (OUT && valid && cp->out_offset >= 0 && a.y_out) ? a.y_out + cp->out_offset
+                                                                   : nullptr;
+    float* gout = (OUT && valid && cp->gain_offset >= 0 && a.g_out) ? a.g_out + cp->gain_offset
+                                                                    : nullptr;
+    const float lg2_floor = (ALGO == CSE_ALGO_OMLSA) ? fast_log2(p2) : 0.0f;
+    const float q_spp = fminf(fmaxf(p3, 1e-3f), 1.0f - 1e-3f);
+
+    // ---- pass-1 twiddles e^{2πi i b/M}, [b][i], shared by the workgroup
+    for (int e = tid; e < 15 * L; e += W::THREADS) {
+        const int b = 1 + e / L, ii = e % L;
+        double s, c;
+        sincospi(2.0 * (double)(ii * b) / (double)M, &s, &c);
+        ((cf*)(smem + W::OFF_TW))[e] = cmk((float)c, (float)s);
+    }
+
+    // ---- row staging: thread tid owns Y/N elements tid + k*THREADS and clean[tid]
+    float2 py[W::YPT];
+    float pn[W::YPT];
+    float pc = 0.0f;
+    auto load_rows = [&](int t) {  // issue loads of frame t's rows into registers
+        if (t < nf) {
+#pragma unroll
+            for (int u = 0; u < W::YPT; ++u) {
+                const int k = tid + u * W::THREADS;
+                if (k < B) {
+                    py[u] = Ybase[t * B + k];
+                    if (nstride) pn[u] = Nbase[t * (int)nstride + k];
+                }
+            }
+        }
+        if (tid < HOP) {
+            const int o = t * HOP - NFFT / 2 + tid;
+            pc = (cbase && o >= 0 && o < len) ? (float)cbase[o] : 0.0f;
+        }
+    };
+    auto store_rows = [&](int t) {  // registers -> LDS rows of frame t
+        if (t < nf) {
+#pragma unroll
+            for (int u = 0; u < W::YPT; ++u) {
+                const int k = tid + u * W::THREADS;
+                if (k < B) {
+                    yrow[k] = py[u];
+                    if (nstride) nrow[k] = pn[u];
+                }
+            }
+        }
+        if (tid < HOP) crow[(t & 1) * W::HMAX + tid] = pc;
+    };
+    if (!nstride) {  // static noise row: once
+        for (int k = tid; k < B; k += W::THREADS) nrow[k] = Nbase[k];
+    }
+    load_rows(0);
+    store_rows(0);
+    load_rows(1);
+
+    // ---- lane constants
+    float bs, bc;  // e^{2πi i/NFFT}
     sincospif(2.0f * (float)i / (float)NFFT, &bs, &bc);
-    const cf base = cmk(bc, bs);
     const int b2 = (L == 16) ? i : (i & 15);
     const int h2 = (L == 16) ? 0 : (i >> 4);
     const int off = 2 * b2 + 32 * h2;  // lane's first sample offset inside a frame
-    float wc[2], ws[2];
+    float wc[2], ws[2], pc2[2], ps2[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
         float s_, c_;
         sincospif(2.0f * (float)(off + e) / (float)NFFT, &s_, &c_);
         wc[e] = (0.5f / NFFT) * c_;
         ws[e] = (0.5f / NFFT) * s_;
+        sincospif(2.0f * (float)(off + e) / 256.0f, &s_, &c_);  // only used for R == 2
+        pc2[e] = c_;
+        ps2[e] = s_;
     }
 
-    // decision-directed state: previous gain / previous a-posteriori SNR
-    // (wiener_filter.py:115-116, mmse.py:62-63, advanced_mmse.py:198-199)
-    // rr = prev_gain**2 * prev_gamma; only read from frame 1 on
-    float rr[17];
+    float rr[17];  // prev_gain**2 * prev_gamma per bin (read from frame 1 on)
 #pragma unroll
     for (int j = 0; j < 17; ++j) rr[j] = 0.0f;
-    const float lg2_floor = fast_log2(algo == CSE_ALGO_OMLSA ? c.p[2] : 1.0f);
-    const float q_spp = fminf(fmaxf(c.p[3], 1e-3f), 1.0f - 1e-3f);
-
     float acc[32];
 #pragma unroll
     for (int q = 0; q < 32; ++q) acc[q] = 0.0f;
@@ -278,24 +336,52 @@ __device__ void run_cells(const Args& a, const LaneCell& c, int algo, cf* lds, c
     bool fin = true;
 
     for (int t = 0; t < nf + R - 1; ++t) {
+        // Keep the lane rotors opaque per frame: otherwise LICM hoists the 32
+        // window values and 16 packing twiddles derived from them out of the
+        // loop (64 live VGPRs, spills).  Recomputing them costs ~130 FMAs/frame.
+        asm volatile("" : "+v"(bc), "+v"(bs), "+v"(wc[0]), "+v"(wc[1]), "+v"(ws[0]),
+                     "+v"(ws[1]), "+v"(pc2[0]), "+v"(pc2[1]), "+v"(ps2[0]), "+v"(ps2[1]));
+        const cf base = cmk(bc, bs);
         if (t < nf) {
-            // ---------------- gain stage: S = Y * G straight into LDS ------
-            __syncthreads();  // previous frame's transpose reads are done
-            switch (algo) {
-                case CSE_ALGO_SS:
-                    gain_stage<CSE_ALGO_SS, NFFT>(c, i, t, rr, lg2_floor, q_spp, sb);
-                    break;
-                case CSE_ALGO_WIENER:
-                    gain_stage<CSE_ALGO_WIENER, NFFT>(c, i, t, rr, lg2_floor, q_spp, sb);
-                    break;
-                case CSE_ALGO_MMSE:
-                    gain_stage<CSE_ALGO_MMSE, NFFT>(c, i, t, rr, lg2_floor, q_spp, sb);
-                    break;
-                default:
-                    gain_stage<CSE_ALGO_OMLSA, NFFT>(c, i, t, rr, lg2_floor, q_spp, sb);
-                    break;
+            __syncthreads();  // rows(t) visible; last frame's transpose reads done
+            // ---------------- gain stage: S = Y * G into my cell's LDS row
+#pragma unroll
+            for (int j = 0; j < 17; ++j) {
+                if (j == 16 && i != 0) continue;
+                const int k = (j < 16) ? i + L * j : M;
+                const float2 y = yrow[k];
+                const float nz = nrow[k];
+                const float P = y.x * y.x + y.y * y.y;
+                float g;
+                cf Sj;
+                if (ALGO == CSE_ALGO_SS) {
+                    // Ps = max(P - a N, b N); |S| = sqrt(Ps) with the noisy phase
+                    // (spectral_subtractor.py:44-53).  No eps floor: the
+                    // reference floors BEFORE fix_length (engine.noise_key).
+                    const float ps = fmaxf(P - p0 * nz, p1 * nz);
+                    const float sp = __builtin_amdgcn_sqrtf(ps);
+                    if (P > 0.0f) {
+                        g = sp * __builtin_amdgcn_rsqf(P);
+                        Sj = cmk(y.x * g, y.y * g);
+                    } else {  // angle(0) = 0
+                        g = 0.0f;
+                        Sj = cmk(sp, 0.0f);
+                    }
+                } else {
+                    if (ALGO == CSE_ALGO_WIENER)
+                        g = gain_wiener(P, nz, t == 0, rr[j], p0, p1);
+                    else if (ALGO == CSE_ALGO_MMSE)
+                        g = gain_mmse(P, nz, t == 0, rr[j], p0, p1, p2, p3);
+                    else
+                        g = gain_omlsa(P, nz, t == 0, rr[j], p0, p1, p2, lg2_floor, q_spp, p4);
+                    Sj = cmk(y.x * g, y.y * g);
+                }
+                sb[k] = Sj;
+                if (OUT && gout) gout[t * B + k] = g;
             }
-            __syncthreads();
+            __syncthreads();  // S rows complete; every wave is done with yrow/nrow(t)
+            store_rows(t + 1);
+            load_rows(t + 2);
 
             // ---------------- pass 1: real-IFFT packing + DFT16 over j -----
             // Z'[k] = (X_k + X*_{M-k}) + i (X_k - X*_{M-k}) e^{2πi k/NFFT}
@@ -315,22 +401,24 @@ __device__ void run_cells(const Args& a, const LaneCell& c, int algo, cf* lds, c
             }
             idft16(z);
 #pragma unroll
-            for (int b = 1; b < 16; ++b) z[b] = cmul(z[b], tw1[b * L + i]);
-            __syncthreads();  // all S reads done before the transpose overwrites
+            for (int b = 1; b < 16; ++b) z[b] = cmul(z[b], tw1[(b - 1) * L + i]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();  // my wave's S reads done (in-order LDS)
 #pragma unroll
-            for (int b = 0; b < 16; ++b) tb[b * G::TROW + i] = z[b];
-            __syncthreads();
+            for (int b = 0; b < 16; ++b) tb[b * L + (i ^ tswz<L>(b))] = z[b];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();  // transpose block complete
 
             // ---------------- pass 2: DFT over the lane index --------------
             cf v[16];
             if (L == 16) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] = tb[i * G::TROW + r];
+                for (int r = 0; r < 16; ++r) v[r] = tb[i * L + (r ^ tswz<L>(i))];
             } else {  // DFT32 = butterfly (lo +- hi) * W32^{r h}, then DFT16
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const cf lo = tb[b2 * G::TROW + r];
-                    const cf hi = tb[b2 * G::TROW + r + 16];
+                    const cf lo = tb[b2 * L + (r ^ tswz<L>(b2))];
+                    const cf hi = tb[b2 * L + ((r + 16) ^ tswz<L>(b2))];
                     const cf u = h2 ? csub(lo, hi) : cadd(lo, hi);
                     v[r] = h2 ? cmul(u, cmk(Rot32::c[r], Rot32::s[r])) : u;
                 }
@@ -340,28 +428,66 @@ __device__ void run_cells(const Args& a, const LaneCell& c, int algo, cf* lds, c
             // ---------------- synthesis window (/n_fft) + overlap-add ------
 #pragma unroll
             for (int q = 0; q < 32; ++q) {
-                const int av = q >> 1, e = q & 1;
-                const float ca = Rot32::c[(2 * av) & 31], sa = Rot32::s[(2 * av) & 31];
-                const float w = 0.5f / NFFT - (ca * wc[e] - sa * ws[e]);
-                const float x = e ? v[av].y : v[av].x;
+                const float w = hann_at<NFFT>(q >> 1, q & 1, wc, ws);
+                const float x = (q & 1) ? v[q >> 1].y : v[q >> 1].x;
                 acc[q] = fmaf(x, w, acc[q]);
             }
+        } else {
+            __syncthreads();  // flush frames: clean row t visible, row t-1 reads done
+            store_rows(t + 1);
+            load_rows(t + 2);
         }
 
         // ---------------- retire HOP finished samples ----------------------
+        // y = ola / wss (librosa istft normalisation), then the SNR error sum
+        // of the clipped sample (evaluation_metrics.py:52-56).  Steady frames
+        // use the closed-form wss; the first R-1 and the flush frames sum the
+        // covering windows explicitly.
+        const float* crow_t = crow + (t & 1) * W::HMAX;
+        float inv_w[F];
+        if ((t < R - 1) || (t >= nf)) {
 #pragma unroll
-        for (int q = 0; q < F; ++q) {
-            const int64_t o = (int64_t)t * HOP + SP * (q >> 1) + off + (q & 1) - NFFT / 2;
-            if (c.valid && o >= 0 && o < len) {
-                const float y = acc[q] * invw[o];
-                fin = fin && __builtin_isfinite(y);
-                if (c.out) c.out[o] = y;
-                if (c.clean) {
-                    const float yc = fminf(fmaxf(y, -1.0f), 1.0f);
-                    const double d = c.clean[o] - (double)yc;
-                    sse = fma(d, d, sse);
+            for (int q = 0; q < F; ++q) {
+                float wss = 0.0f;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int tr = t - r;
+                    if (tr >= 0 && tr < nf) {
+                        const float w = hann_at<NFFT>((q >> 1) + r * (HOP / SP), q & 1, wc, ws) * NFFT;
+                        wss = fmaf(w, w, wss);
+                    }
+                }
+                inv_w[q] = wss > 0.0f ? __builtin_amdgcn_rcpf(wss) : 1.0f;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < F; ++q) {
+                if (R == 2) {
+                    // 0.75 + 0.25 cos(2π n/256) for 512/256; n = 32 aq + off + e
+                    const int m = (4 * (q >> 1)) & 31;  // 2π(32 aq)/256 = 2π(4 aq)/32
+                    inv_w[q] = __builtin_amdgcn_rcpf(
+                        0.75f + 0.25f * (Rot32::c[m] * pc2[q & 1] - Rot32::s[m] * ps2[q & 1]));
+                } else {
+                    inv_w[q] = (R == 4) ? (1.0f / 1.5f) : (1.0f / 3.0f);
                 }
             }
+        }
+        if (valid) {
+            const int o0 = t * HOP + off - NFFT / 2;  // output index of q = 0
+            float part = 0.0f;
+#pragma unroll
+            for (int q = 0; q < F; ++q) {
+                const int n = SP * (q >> 1) + (q & 1);  // + off: position inside frame t
+                const int o = o0 + n;
+                if (o >= 0 && o < len) {
+                    const float y = acc[q] * inv_w[q];
+                    fin = fin && __builtin_isfinite(y);
+                    if (OUT && yout) yout[o] = y;
+                    const float d = crow_t[n + off] - fminf(fmaxf(y, -1.0f), 1.0f);
+                    part = fmaf(d, d, part);
+                }
+            }
+            sse += (double)part;
         }
 #pragma unroll
         for (int q = 0; q < 32 - F; ++q) acc[q] = acc[q + F];
@@ -374,53 +500,44 @@ __device__ void run_cells(const Args& a, const LaneCell& c, int algo, cf* lds, c
     for (int m = L / 2; m > 0; m >>= 1) sse += __shfl_xor(sse, m, 64);
     const unsigned long long bad = __ballot(!fin);
     const unsigned long long my = (bad >> (cs * L)) & ((1ull << L) - 1);
-    if (i == 0 && c.valid) {
+    const int64_t cell_idx = (int64_t)(wcell - a.cells) + cslot;
+    if (i == 0 && valid) {
         if (a.sse) a.sse[cell_idx] = sse;
         if (a.finite) a.finite[cell_idx] = my == 0 ? 1 : 0;
     }
 }
 
-template <int NFFT>
-__global__ void __launch_bounds__(64) enhance_kernel(Args a) {
-    using G = Geo<NFFT>;
-    __shared__ __attribute__((aligned(16))) cf lds[G::REGION];
-    __shared__ __attribute__((aligned(16))) cf tw1[16 * G::L];
-    const int lane = threadIdx.x;
-    // pass-1 twiddles e^{2πi i b/M}, [b][i]
-    for (int e = lane; e < 16 * G::L; e += 64) {
-        const int b = e / G::L, ii = e % G::L;
-        double s, c;
-        sincospi(2.0 * (double)(ii * b) / (double)G::M, &s, &c);
-        tw1[e] = cmk((float)c, (float)s);
+template <int NFFT, int HOP, bool OUT>
+__device__ __forceinline__ void dispatch_algo(const Args& a, const cse_cell_t* wcell, int n,
+                                              int algo, unsigned char* smem) {
+    switch (algo) {
+        case CSE_ALGO_SS: run_wg<NFFT, HOP, CSE_ALGO_SS, OUT>(a, wcell, n, smem); break;
+        case CSE_ALGO_WIENER: run_wg<NFFT, HOP, CSE_ALGO_WIENER, OUT>(a, wcell, n, smem); break;
+        case CSE_ALGO_MMSE: run_wg<NFFT, HOP, CSE_ALGO_MMSE, OUT>(a, wcell, n, smem); break;
+        case CSE_ALGO_OMLSA: run_wg<NFFT, HOP, CSE_ALGO_OMLSA, OUT>(a, wcell, n, smem); break;
+        default: break;
     }
-    __syncthreads();
-    const int wave = xcd_remap(blockIdx.x, gridDim.x);
-    const int cs = lane / G::L;
-    const int64_t first = (int64_t)wave * G::CPW;
-    const int64_t ci = first + cs;
-    LaneCell c;
-    const cse_cell_t* cp = a.cells + (ci < a.n_cells ? ci : first);
-    c.algo = cp->algo;
-    c.valid = (ci < a.n_cells) && c.algo >= 0;
-    if (!c.valid) c.algo = CSE_ALGO_NONE;
-    c.Y = a.Y + cp->y_offset;
-    c.N = a.noise + cp->noise_offset;
-    c.nstride = cp->noise_stride;
-    c.clean = (c.valid && cp->clean_offset >= 0 && a.clean) ? a.clean + cp->clean_offset : nullptr;
-    c.out = (c.valid && cp->out_offset >= 0 && a.y_out) ? a.y_out + cp->out_offset : nullptr;
-    c.gout = (c.valid && cp->gain_offset >= 0 && a.g_out) ? a.g_out + cp->gain_offset : nullptr;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) c.p[k] = cp->param[k];
-    // hop and algorithm are the first slot's (the host packs equal hop/algo per
-    // wave); a slot that disagrees is skipped (finite = 0 never written: host
-    // validates packing before launch).
-    const int hop = __builtin_amdgcn_readfirstlane(a.cells[first].hop);
-    const int algo = __builtin_amdgcn_readfirstlane(a.cells[first].algo);
-    if (c.valid && (cp->hop != hop || c.algo != algo)) c.valid = false;
+}
+
+// OUT: the y_out / g_out variant (parity tests, single-cell plugin calls);
+// the grid/bench path computes only the per-cell score sums.
+template <int NFFT, bool OUT>
+__global__ void __launch_bounds__(256, CSE_WAVES_PER_SIMD) enhance_kernel(Args a) {
+    using W = WG<NFFT>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t first = (int64_t)wg * W::CPWG;
+    const int64_t left = a.n_cells - first;
+    const int n = (int)(left < W::CPWG ? left : W::CPWG);
+    const cse_cell_t* wcell = a.cells + first;
+    // hop and algorithm of the workgroup = its first cell's (host packs so);
+    // slots of another algorithm are skipped (finite never set).
+    const int hop = __builtin_amdgcn_readfirstlane(wcell[0].hop);
+    const int algo = __builtin_amdgcn_readfirstlane(wcell[0].algo);
     if (hop == 128)
-        run_cells<NFFT, 128>(a, c, algo, lds, tw1, ci);
+        dispatch_algo<NFFT, 128, OUT>(a, wcell, n, algo, smem);
     else if (hop == 256)
-        run_cells<NFFT, 256>(a, c, algo, lds, tw1, ci);
+        dispatch_algo<NFFT, 256, OUT>(a, wcell, n, algo, smem);
 }
 
 }  // namespace cse
@@ -429,13 +546,12 @@ using namespace cse;
 
 extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
                                  const float* Y, const float* noise, const double* clean,
-                                 const float* inv_wss128, const float* inv_wss256, float* y_out,
-                                 float* g_out, double* sse, uint8_t* finite,
+                                 float* y_out, float* g_out, double* sse, uint8_t* finite,
                                  cse_stream_t stream) {
     CSE_CHECK_ARG(n_fft == 512 || n_fft == 1024, "cse_enhance_cells: n_fft=%d (512|1024)", n_fft);
     CSE_CHECK_ARG(cells && Y && noise, "cse_enhance_cells: NULL cells/Y/noise");
-    CSE_CHECK_ARG(len >= 1 && n_cells >= 0, "cse_enhance_cells: len=%lld n_cells=%lld",
-                  (long long)len, (long long)n_cells);
+    CSE_CHECK_ARG(len >= 1 && len < (1ll << 30) && n_cells >= 0,
+                  "cse_enhance_cells: len=%lld n_cells=%lld", (long long)len, (long long)n_cells);
     if (n_cells == 0) return CSE_OK;
     Args a;
     a.len = len;
@@ -444,21 +560,33 @@ extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells
     a.Y = (const float2*)Y;
     a.noise = noise;
     a.clean = clean;
-    a.inv_wss128 = inv_wss128;
-    a.inv_wss256 = inv_wss256;
     a.y_out = y_out;
     a.g_out = g_out;
     a.sse = sse;
     a.finite = finite;
-    const int cpw = CSE_CELLS_PER_WAVE(n_fft);
-    const int64_t waves = (n_cells + cpw - 1) / cpw;
-    CSE_CHECK_ARG(waves < (1ll << 31), "cse_enhance_cells: too many cells");
-    if (n_fft == 512)
-        hipLaunchKernelGGL(enhance_kernel<512>, dim3((unsigned)waves), dim3(64), 0,
-                           (hipStream_t)stream, a);
-    else
-        hipLaunchKernelGGL(enhance_kernel<1024>, dim3((unsigned)waves), dim3(64), 0,
-                           (hipStream_t)stream, a);
+    const int per = CSE_CELLS_PER_GROUP(n_fft);
+    const int64_t groups = (n_cells + per - 1) / per;
+    CSE_CHECK_ARG(groups < (1ll << 31), "cse_enhance_cells: too many cells");
+    const bool out = (y_out != nullptr) || (g_out != nullptr);
+    const void* fn;
+    int bytes;
+    if (n_fft == 512) {
+        fn = out ? (const void*)enhance_kernel<512, true> : (const void*)enhance_kernel<512, false>;
+        bytes = WG<512>::BYTES;
+    } else {
+        fn = out ? (const void*)enhance_kernel<1024, true> : (const void*)enhance_kernel<1024, false>;
+        bytes = WG<1024>::BYTES;
+    }
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) {
+        ::cse::set_error("cse_enhance_cells: cannot reserve %d bytes of LDS", bytes);
+        return CSE_ELAUNCH;
+    }
+    void* args[] = {&a};
+    if (hipLaunchKernel(fn, dim3((unsigned)groups), dim3(256), args, (size_t)bytes,
+                        (hipStream_t)stream) != hipSuccess) {
+        ::cse::set_error("cse_enhance_cells: launch failed");
+        return CSE_ELAUNCH;
+    }
     CSE_CHECK_LAUNCH("cse_enhance_cells");
     return CSE_OK;
 }

@@ -6,7 +6,6 @@ every numeric step is a libcse.so kernel (include/cse.h):
   cse_stft            STFT of every signal at each (n_fft, hop)        [once per group]
   cse_noise_estimate  percentile / min-tracking / true-noise PSDs     [once per group]
   cse_noise_smooth    MMSE/OMLSA noise IIR (per noise_mu)             [once per group]
-  cse_istft_norm      1/window-sum-square per (n_fft, hop)            [once]
   cse_enhance_cells   THE HOT PATH: gain recursion + ISTFT + SNR sums [per grid cell]
 
 A "cell spec" is (signal index, algorithm name, params dict) where params are
@@ -223,7 +222,6 @@ class GridPlan:
         Tmax = max(n_frames(L, h) for h in self.hops)
         self.ws = torch.empty(int(eng.lib.cse_noise_workspace_bytes(S, Tmax, B)),
                               dtype=torch.uint8, device=dev)
-        self.inv = {h: eng.istft_norm(n_fft, h, L) for h in self.hops}
         # ---- cell table
         cells = np.zeros(len(items), dtype=_lib.CELL_DTYPE)
         g_total = 0
@@ -301,7 +299,7 @@ class GridPlan:
         """THE HOT PATH launch: every cell of this n_fft, one kernel."""
         _lib.check(self.eng.lib.cse_enhance_cells(
             self.n_fft, self.L, _ptr(self.cells_d), self.n_packed, _ptr(self.Ybuf),
-            _ptr(self.pool), _ptr(self.clean), _ptr(self.inv.get(128)), _ptr(self.inv.get(256)),
+            _ptr(self.pool), _ptr(self.clean),
             _ptr(self.y_all), _ptr(self.g_out), _ptr(self.sse_d), _ptr(self.fin_d), _stream()),
             "cse_enhance_cells")
 
@@ -372,43 +370,43 @@ class MultiPlan:
 
 
 def pack_waves(cells, n_fft):
-    """Group cells that share (hop, algo, spectrum, noise) into wave slots.
+    """Group cells into workgroup slot groups (CSE_CELLS_PER_GROUP cells each).
 
-    Returns (packed cells incl. CSE_ALGO_NONE padding, order) where
-    order[i] = index into ``cells`` of packed slot i, or -1 for padding.
-    Waves are ordered longest-first (frames x algorithm cost) so the tail of the
-    launch is short waves; groups stay contiguous so the kernel's XCD remap
-    keeps a group's Y/N rows in one XCD's L2.
+    A slot group's cells must share (algo, hop, spectrum, noise, clean) — the
+    kernel stages those rows once per workgroup.  Returns (packed cells incl.
+    CSE_ALGO_NONE padding, order) with order[i] = index into ``cells`` of packed
+    slot i, or -1 for padding.  Groups are ordered longest-first (frames x
+    algorithm cost) so the launch ends on short workgroups; neighbours share
+    rows, and the kernel's XCD remap keeps neighbours on one XCD's L2.
     """
-    cpw = _lib.cells_per_wave(n_fft)
+    per = _lib.cells_per_group(n_fft)
     code_name = {v: k for k, v in _lib.ALGO.items()}
     groups = {}
     for i, c in enumerate(cells):
-        key = (int(c["hop"]), int(c["algo"]), int(c["y_offset"]), int(c["noise_offset"]))
+        key = (int(c["hop"]), int(c["algo"]), int(c["y_offset"]), int(c["noise_offset"]),
+               int(c["noise_stride"]), int(c["clean_offset"]))
         groups.setdefault(key, []).append(i)
-    waves = []
+    slots = []
     for key, idxs in groups.items():
         hop, algo = key[0], key[1]
         cost = (1 + 16000 // hop) * ALGO_COST[code_name[algo]]
-        for s in range(0, len(idxs), cpw):
-            chunk = idxs[s:s + cpw]
-            waves.append((-cost, key, chunk + [-1] * (cpw - len(chunk))))
-    waves.sort(key=lambda w: (w[0], w[1]))
-    order = np.array([i for w in waves for i in w[2]], dtype=np.int64)
+        for s in range(0, len(idxs), per):
+            chunk = idxs[s:s + per]
+            slots.append((-cost, key, chunk + [-1] * (per - len(chunk))))
+    slots.sort(key=lambda w: (w[0], w[1]))
+    order = np.array([i for w in slots for i in w[2]], dtype=np.int64)
     packed = np.zeros(len(order), dtype=_lib.CELL_DTYPE)
     real = order >= 0
     packed[real] = cells[order[real]]
-    # padding slots: same hop/algo as their wave (kernel skips them)
-    for w, (_, key, chunk) in enumerate(waves):
+    for g, (_, key, chunk) in enumerate(slots):
         for s, i in enumerate(chunk):
-            if i < 0:
-                slot = w * cpw + s
+            if i < 0:  # padding: same shared rows, no algorithm, no outputs
+                slot = g * per + s
                 packed[slot] = cells[chunk[0]]
                 packed[slot]["algo"] = -1
                 packed[slot]["out_offset"] = -1
                 packed[slot]["gain_offset"] = -1
-    # a padded slot's algo = -1 would become the wave algo only if it were slot 0
-    assert all(packed[w * cpw]["algo"] >= 0 for w in range(len(waves)))
+    assert all(packed[g * per]["algo"] >= 0 for g in range(len(slots)))
     return packed, order
 
 

@@ -60,10 +60,11 @@ enum {
 
 /*
  * One grid cell = one (signal group, noise PSD, algorithm, parameter set).
- * Cells are processed CSE_CELLS_PER_WAVE(n_fft) at a time by one wavefront;
- * all cells of such a slot group must have the same `hop` (pad with
- * CSE_ALGO_NONE slots).  Cells of one slot group that also share `y_offset`
- * and `noise_offset` share their global loads (fastest).
+ * Cells are processed CSE_CELLS_PER_GROUP(n_fft) at a time by one 256-thread
+ * workgroup (4 wavefronts) that stages their shared rows in LDS, so the cells
+ * of one such slot group (cells[g*G .. g*G+G-1]) MUST share algo, hop,
+ * y_offset, noise_offset, noise_stride and clean_offset; pad a short group
+ * with CSE_ALGO_NONE slots.  Only param, out_offset and gain_offset may differ.
  */
 typedef struct cse_cell {
     int32_t algo;          /* CSE_ALGO_* */
@@ -71,13 +72,13 @@ typedef struct cse_cell {
     int64_t y_offset;      /* offset (in complex elements) of this cell's spectrum Y[T][B] */
     int64_t noise_offset;  /* offset (floats) of this cell's noise PSD */
     int64_t noise_stride;  /* floats between frames of the noise PSD: 0 = static [B], B = [T][B] */
-    int64_t clean_offset;  /* offset (floats) of the clean reference for the SNR, or -1 */
+    int64_t clean_offset;  /* offset (doubles) of the clean reference for the SNR, or -1 */
     int64_t out_offset;    /* offset (floats) of this cell's output waveform in y_out, or -1 */
     int64_t gain_offset;   /* offset (floats) of this cell's gain matrix G[T][B] in g_out, or -1 */
     float param[8];        /* algorithm parameters, order as in the CSE_ALGO_* comments */
 } cse_cell_t;              /* 88 bytes */
 
-#define CSE_CELLS_PER_WAVE(n_fft) ((n_fft) == 512 ? 4 : 2)
+#define CSE_CELLS_PER_GROUP(n_fft) ((n_fft) == 512 ? 16 : 8)
 
 /* Library identity. */
 int cse_version(void);
@@ -127,7 +128,8 @@ int cse_noise_smooth(const float* N, int64_t n_sig, int T, int B, int src_frames
 /*
  * 1 / window-sum-square of the ISTFT (librosa 0.11 istft normalisation) for a
  * centred signal of `len` samples; entries where the sum is <= DBL_MIN are 1.
- * out: [len] f32.
+ * out: [len] f32.  (A reference table: cse_enhance_cells computes the same
+ * normalisation analytically in-kernel.)
  */
 int cse_istft_norm(int n_fft, int hop, int64_t len, float* out, cse_stream_t stream);
 
@@ -142,13 +144,10 @@ int cse_istft_norm(int n_fft, int hop, int64_t len, float* out, cse_stream_t str
  *   finite[c] = 1 if every y[n] is finite
  * Optional outputs: y_out (the enhanced waveform, f32, [len] at out_offset)
  * and g_out (the gain matrix, f32 [T][B] at gain_offset).
- * inv_wss128 / inv_wss256: cse_istft_norm tables for hop 128 / 256 (each may
- * be NULL if no cell uses that hop).
  * n_fft in {512, 1024}; hop in {128, 256}.
  */
 int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
                       const float* Y, const float* noise, const double* clean,
-                      const float* inv_wss128, const float* inv_wss256,
                       float* y_out, float* g_out, double* sse, uint8_t* finite,
                       cse_stream_t stream);
 

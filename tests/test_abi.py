@@ -41,8 +41,7 @@ def test_version_and_error_channel(lib):
     rc = lib.cse_stft(ctypes.c_void_p(16), None, 1, 100, 500, 128, None, None, None)
     assert rc == -1 and b"n_fft" in lib.cse_last_error()
     rc = lib.cse_enhance_cells(256, 100, ctypes.c_void_p(16), 1, ctypes.c_void_p(16),
-                               ctypes.c_void_p(16), None, None, None, None, None, None, None,
-                               None)
+                               ctypes.c_void_p(16), None, None, None, None, None, None)
     assert rc == -1 and b"n_fft" in lib.cse_last_error()
     rc = lib.cse_noise_estimate(7, ctypes.c_void_p(16), 1, 100, 257, 20.0, 1e-10,
                                 ctypes.c_void_p(16), ctypes.c_void_p(16), None)
@@ -67,12 +66,13 @@ def test_wave_packing_groups_and_pads():
     cells["hop"] = [128, 128, 256, 128, 128, 128, 128]
     cells["y_offset"] = [0, 0, 5, 0, 0, 0, 0]
     packed, order = pack_waves(cells, 512)
-    assert len(packed) % 4 == 0
+    assert len(packed) % 16 == 0
     assert sorted(order[order >= 0].tolist()) == list(range(7))
-    for w in range(len(packed) // 4):
-        slots = packed[4 * w:4 * w + 4]
+    for w in range(len(packed) // 16):
+        slots = packed[16 * w:16 * w + 16]
         real = slots[slots["algo"] >= 0]
-        assert len(set(real["hop"].tolist())) == 1 and len(set(real["algo"].tolist())) == 1
+        for f in ("hop", "algo", "y_offset", "noise_offset", "noise_stride", "clean_offset"):
+            assert len(set(slots[f].tolist() if f != "algo" else real[f].tolist())) == 1, f
         assert slots[0]["algo"] >= 0
     # longest first: hop 128 OMLSA before hop 128 SS and hop 256 OMLSA
     assert packed[0]["algo"] == 3 and packed[0]["hop"] == 128
