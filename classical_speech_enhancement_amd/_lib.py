@@ -25,12 +25,13 @@ CELL_DTYPE = np.dtype([
 assert CELL_DTYPE.itemsize == 88
 
 EXPORTS = ("cse_version", "cse_last_error", "cse_stft", "cse_noise_workspace_bytes",
-           "cse_noise_estimate", "cse_noise_smooth", "cse_istft_norm", "cse_enhance_cells")
+           "cse_noise_estimate", "cse_noise_smooth", "cse_noise_invert", "cse_istft_norm",
+           "cse_enhance_cells")
 
 
 def cells_per_group(n_fft):
-    """Cells per 256-thread workgroup slot group (CSE_CELLS_PER_GROUP)."""
-    return 16 if n_fft == 512 else 8
+    """Cells per workgroup slot group (CSE_CELLS_PER_GROUP)."""
+    return 12 if n_fft == 512 else 6
 
 
 class CseError(RuntimeError):
@@ -62,6 +63,8 @@ def load(path=LIB_PATH):
     lib.cse_noise_estimate.argtypes = [i32, P, i64, i32, i32, f64, f64, P, P, P]
     lib.cse_noise_smooth.restype = i32
     lib.cse_noise_smooth.argtypes = [P, i64, i32, i32, i32, f64, P, P]
+    lib.cse_noise_invert.restype = i32
+    lib.cse_noise_invert.argtypes = [P, i64, f64, P, P]
     lib.cse_istft_norm.restype = i32
     lib.cse_istft_norm.argtypes = [i32, i32, i64, P, P]
     lib.cse_enhance_cells.restype = i32

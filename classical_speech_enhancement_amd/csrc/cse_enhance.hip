@@ -71,8 +71,8 @@ constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
 // exp(-v/2)[(1+v)I0(v/2) + v I1(v/2)] for v in [1e-12, 80]
-__device__ __forceinline__ float mmse_bracket_over_sqrtv_times(float v, float sqrtv) {
-    // returns h(v) (not divided): v<=4 -> PA(t); v>4 -> sqrt(v)*PB(t(1/v))
+__device__ __forceinline__ float mmse_bracket(float v, float sqrtv) {
+    // v<=4 -> PA(t); v>4 -> sqrt(v)*PB(t(1/v))
     const float ta = (v - 2.0f) * 0.5f;
     const float u = fast_rcp(v);
     const float tb = (2.0f * u - (CSE_HB_U0 + CSE_HB_U1)) * (1.0f / (CSE_HB_U1 - CSE_HB_U0));
@@ -81,46 +81,35 @@ __device__ __forceinline__ float mmse_bracket_over_sqrtv_times(float v, float sq
     return v <= 4.0f ? pa : sqrtv * pb;
 }
 
-// E1(v) = expn(1, v) for v in [1e-12, 80]; exp_v = exp(v) (shared with the SPP term)
-__device__ __forceinline__ float expint_e1(float v, float exp_v) {
-    const float small = -0.5772156649015329f - fast_log2(v) * kLn2 + v * horner(CSE_EIN, v);
-    const float u = fast_rcp(v);
-    const float te = (2.0f * u - (1.0f / 80.0f + 1.0f)) * (1.0f / (1.0f - 1.0f / 80.0f));
-    const float large = fast_rcp(exp_v) * u * horner(CSE_E1L, te);
-    return v <= 1.0f ? small : large;
-}
-
 // ---------------------------------------------------------------------------
-// per-bin gains.  P = |Y|^2, N = noise PSD of this frame/bin.  gp/gm = the
-// decision-directed state (previous gain / previous a-posteriori SNR).
+// per-bin gains.  P = |Y|^2; inv = 1/max(N, eps) prepared per noise row by the
+// host-side pipeline (cse_noise_invert), so gamma = max(P*inv, eps) exactly as
+// max(P/max(N,eps), eps) up to one rounding.  The decision-directed recursion
+// only ever uses prev_gain**2 * prev_gamma (wiener_filter.py:133, mmse.py:82,
+// advanced_mmse.py:215): the carried state is rr = (G*G)*gamma.
 // ---------------------------------------------------------------------------
-// The decision-directed recursion only ever uses prev_gain**2 * prev_gamma
-// (wiener_filter.py:133, mmse.py:82, advanced_mmse.py:215), so the carried
-// state is that one product, rr = (G*G)*gamma, evaluated in the reference order.
-__device__ __forceinline__ float gain_wiener(float P, float N, bool first, float& rr,
+__device__ __forceinline__ float gain_wiener(float P, float inv, bool first, float& rr,
                                              float alpha, float gfloor) {
-    const float n = fmaxf(N, 1e-10f);
-    const float gam = fmaxf(__fdividef(P, n), 1e-10f);
+    const float gam = fmaxf(P * inv, 1e-10f);
     const float d = fmaxf(gam - 1.0f, 0.0f);
     float xi = first ? d : alpha * rr + (1.0f - alpha) * d;
     xi = fmaxf(xi, 1e-10f);
-    const float g = fminf(fmaxf(__fdividef(xi, 1.0f + xi), gfloor), 1.0f);
+    const float g = fminf(fmaxf(xi * fast_rcp(1.0f + xi), gfloor), 1.0f);
     rr = (g * g) * gam;
     return g;
 }
 
-__device__ __forceinline__ float gain_mmse(float P, float N, bool first, float& rr,
+__device__ __forceinline__ float gain_mmse(float P, float inv, bool first, float& rr,
                                            float alpha, float ksi_min, float gmin, float gmax) {
-    const float n = fmaxf(N, 1e-12f);
-    const float gam = fmaxf(__fdividef(P, n), 1e-12f);
+    const float gam = fmaxf(P * inv, 1e-12f);
     float xi;
     if (first)
         xi = fmaxf(gam - 1.0f, ksi_min);
     else
         xi = fmaxf(alpha * rr + (1.0f - alpha) * fmaxf(gam - 1.0f, 0.0f), ksi_min);
-    const float v = fminf(fmaxf(__fdividef(xi * gam, 1.0f + xi), 1e-12f), 80.0f);
-    const float sv = __builtin_sqrtf(v);
-    const float h = mmse_bracket_over_sqrtv_times(v, sv);
+    const float v = fminf(fmaxf(xi * gam * fast_rcp(1.0f + xi), 1e-12f), 80.0f);
+    const float sv = __builtin_amdgcn_sqrtf(v);
+    const float h = mmse_bracket(v, sv);
     float g = (0.88622692545275801f * (sv * fast_rcp(gam + 1e-12f))) * h;
     if (__builtin_isnan(g)) g = gmin;
     if (__builtin_isinf(g)) g = g > 0.0f ? gmax : gmin;
@@ -129,11 +118,16 @@ __device__ __forceinline__ float gain_mmse(float P, float N, bool first, float& 
     return g;
 }
 
-__device__ __forceinline__ float gain_omlsa(float P, float N, bool first, float& rr,
+// Log-MMSE x speech-presence gain (advanced_mmse.py:100-121), in the log2 domain:
+//   log2 g_lsa = log2(xi/(1+xi)) + 0.5 log2(e) E1(v),  E1 = Ein(v) - ln v - gamma_E
+//             = log2(xi r / sqrt(v)) + 0.5 log2(e) (Ein(v) - gamma_E)      (v < 17)
+//             = log2(xi r)                                               (v >= 17: E1 < 2.4e-9)
+//   p = 1/(1 + (1-q)/(q Lambda + eps)) = A / (A + 1 - q),  A = q Lambda + eps
+//   G = clip(g_lsa^p gf^(1-p), gf, 1) = clip(exp2(lgf + p (lg - lgf)), gf, 1)
+__device__ __forceinline__ float gain_omlsa(float P, float inv, bool first, float& rr,
                                             float alpha, float ksi_min, float gfloor,
                                             float lg2_floor, float q, float vmax) {
-    const float n = fmaxf(N, 1e-10f);
-    const float gam = fmaxf(__fdividef(P, n), 1e-10f);
+    const float gam = fmaxf(P * inv, 1e-10f);
     float xi;
     if (first)
         xi = fmaxf(gam - 1.0f, ksi_min);
@@ -141,16 +135,17 @@ __device__ __forceinline__ float gain_omlsa(float P, float N, bool first, float&
         xi = fmaxf(alpha * rr + (1.0f - alpha) * fmaxf(gam - 1.0f, 0.0f), ksi_min);
     const float r = fast_rcp(1.0f + xi);
     const float v = fminf(fmaxf(xi * gam * r, 1e-12f), vmax);
-    const float ev = fast_exp2(v * kLog2e);
-    const float e1 = expint_e1(v, ev);
-    // log2 of g_lsa = xi/(1+xi) * exp(0.5*E1); nan_to_num(nan->gf, +inf->1, -inf->gf)
-    float lg = fast_log2(xi * r) + (0.5f * kLog2e) * e1;
-    if (__builtin_isnan(lg)) lg = lg2_floor;
+    const bool small = v < CSE_EIN_VMAX;
+    const float vc = fminf(v, CSE_EIN_VMAX);
+    const float ein = horner(CSE_EINP, vc * (2.0f / CSE_EIN_VMAX) - 1.0f);
+    const float X = xi * r * (small ? __builtin_amdgcn_rsqf(vc) : 1.0f);
+    float lg = fast_log2(X) + (small ? (0.5f * kLog2e) * (ein - 0.5772156649015329f) : 0.0f);
+    if (__builtin_isnan(lg)) lg = lg2_floor;          // nan_to_num(nan -> gain_floor)
     if (__builtin_isinf(lg)) lg = lg > 0.0f ? 0.0f : lg2_floor;
-    const float lam = r * ev;
-    const float term = __fdividef(1.0f - q, q * lam + 1e-10f);
-    const float p = fminf(fmaxf(fast_rcp(1.0f + term), 0.0f), 1.0f);
-    const float g = fast_exp2(p * lg + (1.0f - p) * lg2_floor);
+    const float ev = fast_exp2(v * kLog2e);
+    const float A = q * (r * ev) + 1e-10f;
+    const float p = fminf(fmaxf(A * fast_rcp(A + (1.0f - q)), 0.0f), 1.0f);
+    const float g = fast_exp2(lg2_floor + p * (lg - lg2_floor));
     const float G = fminf(fmaxf(g, gfloor), 1.0f);
     rr = (G * G) * gam;
     return G;
@@ -167,8 +162,8 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 }
 
 // ---------------------------------------------------------------------------
-// Workgroup = 4 waves = CPWG cells that share hop, algorithm, spectrum Y,
-// noise PSD and clean reference (the host packs them so).  Per frame the
+// Workgroup = 3 waves = CPWG cells that share hop, algorithm, spectrum Y,
+// noise row and clean reference (the host packs them so).  Per frame the
 // workgroup stages the shared rows (Y[t][:], N[t][:], clean[retired samples])
 // into LDS once, cooperatively, one frame ahead (a few VGPRs per thread),
 // instead of every lane keeping 17 bins of loads in flight.
@@ -176,14 +171,16 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 template <int NFFT>
 struct WG {
     using G = Geo<NFFT>;
-    static constexpr int WAVES = 4;
+    static constexpr int WAVES = 3;
     static constexpr int THREADS = 64 * WAVES;
-    static constexpr int CPWG = WAVES * G::CPW;                  // cells per workgroup
+    static constexpr int CPWG = WAVES * G::CPW;                   // cells per workgroup
     static constexpr int HMAX = 256;                              // largest hop
-    // per-cell LDS region: S row (B complex) aliased with the 16 x L transpose;
-    // stride = 64 B mod 256 B so the cells sharing a 32-lane group use
-    // disjoint bank halves in the transposed read.
-    static constexpr int CREG = ((G::B * 8 - 64 + 255) / 256) * 256 + 64;   // bytes
+    static constexpr int TR = G::L + 1;                           // padded transpose row
+    // per-cell LDS region: S row (B complex) aliased with the 16 x (L+1)
+    // transpose block.  16*17*8 = 2176 B = 128 mod 256: the two cells of a
+    // 32-lane group read disjoint bank halves in the transposed read.
+    static constexpr int CREG_RAW = (G::B * 8 > 16 * TR * 8) ? G::B * 8 : 16 * TR * 8;
+    static constexpr int CREG = ((CREG_RAW + 127) / 128) * 128 + (((CREG_RAW + 127) / 128) % 2 ? 0 : 128);
     static constexpr int OFF_CELLS = 0;
     static constexpr int OFF_Y = CPWG * CREG;                     // float2[B]
     static constexpr int OFF_N = OFF_Y + ((G::B * 8 + 15) / 16) * 16;   // float[B]
@@ -191,23 +188,26 @@ struct WG {
     static constexpr int OFF_TW = OFF_C + 2 * HMAX * 4;           // cf[15][L] (b = 1..15)
     static constexpr int BYTES = OFF_TW + 15 * G::L * 8;
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
+    static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
-
-// transposed-block column swizzle (bank-conflict-free reads, see WG::CREG)
 static_assert(WG<512>::BYTES <= 163840 / 4, "n_fft=512 workgroup must fit 4 per CU");
+static_assert(WG<1024>::BYTES <= 163840 / 4, "n_fft=1024 workgroup must fit 4 per CU");
+static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
+              WG<1024>::CPWG == CSE_CELLS_PER_GROUP(1024), "cse.h slot-group size");
 
 // waves per SIMD the register allocation targets (VGPR budget 512 / w)
 #ifndef CSE_WAVES_PER_SIMD
-#define CSE_WAVES_PER_SIMD 2
+#define CSE_WAVES_PER_SIMD 3
 #endif
 
-template <int L>
-__device__ __forceinline__ int tswz(int b) { return L == 16 ? (b >> 1) : b; }
+// hide a value's provenance from the optimiser (keeps derived per-lane
+// addresses/rotors from being hoisted into long-lived registers)
+template <typename T>
+__device__ __forceinline__ T opaque(T x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
 
-// The (fp64-exact) window-sum-square of librosa istft at padded position p is
-// sum_r w^2(n + r*HOP) over the frames that cover p.  With all R frames present
-// it is 1.5 (R=4) / 3 (R=8) for the periodic Hann, or 0.75 + 0.25 cos(2π n/256)
-// for 512/256 (R=2); the first R-1 and the flush frames take the exact sum.
 template <int NFFT>
 __device__ __forceinline__ float hann_at(int aidx, int e, const float (&wc)[2],
                                          const float (&ws)[2]) {
@@ -221,7 +221,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                                        unsigned char* smem) {
     using G = Geo<NFFT>;
     using W = WG<NFFT>;
-    constexpr int M = G::M, L = G::L, B = G::B, SP = G::SP;
+    constexpr int M = G::M, L = G::L, B = G::B, SP = G::SP, TR = W::TR;
     constexpr int R = NFFT / HOP;       // frames overlapping one sample
     constexpr int F = 2 * HOP / SP;     // samples a lane retires per frame
     static_assert(F >= 2 && F <= 32 && (F % 2) == 0, "hop/n_fft combination");
@@ -229,8 +229,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     const int wave = tid >> 6, lane = tid & 63;
     const int cs = lane / L, i = lane % L;
     const int cslot = wave * G::CPW + cs;
-    cf* sb = (cf*)(smem + W::OFF_CELLS + cslot * W::CREG);
-    cf* tb = sb;  // aliased: S row until pass 1 is done, then the transpose block
+    const int creg = W::OFF_CELLS + cslot * W::CREG;   // byte offset of my cell's region
     float2* yrow = (float2*)(smem + W::OFF_Y);
     float* nrow = (float*)(smem + W::OFF_N);
     float* crow = (float*)(smem + W::OFF_C);
@@ -240,19 +239,18 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     const int len = (int)a.len;
     const float2* Ybase = a.Y + wcell[0].y_offset;
     const float* Nbase = a.noise + wcell[0].noise_offset;
-    const int64_t nstride = wcell[0].noise_stride;
+    const int nstride = (int)wcell[0].noise_stride;
     const double* cbase = (a.clean && wcell[0].clean_offset >= 0) ? a.clean + wcell[0].clean_offset
                                                                   : nullptr;
-    // without a clean reference the sums are of y^2 (crow rows stay 0)
-    const int T = 1 + (int)(len / HOP);
-    const int need = (int)((len + NFFT + HOP - 1) / HOP);
+    const int T = 1 + len / HOP;
+    const int need = (len + NFFT + HOP - 1) / HOP;
     const int nf = need < T ? need : T;
 
     // ---- my cell
     const bool valid = cslot < n_cells_wg && wcell[cslot].algo == ALGO;
     const cse_cell_t* cp = wcell + (cslot < n_cells_wg ? cslot : 0);
-    float p0 = cp->param[0], p1 = cp->param[1], p2 = cp->param[2], p3 = cp->param[3],
-          p4 = cp->param[4];
+    const float p0 = cp->param[0], p1 = cp->param[1], p2 = cp->param[2], p3 = cp->param[3],
+                p4 = cp->param[4];
     float* yout = (OUT && valid && cp->out_offset >= 0 && a.y_out) ? a.y_out + cp->out_offset
                                                                    : nullptr;
     float* gout = (OUT && valid && cp->gain_offset >= 0 && a.g_out) ? a.g_out + cp->gain_offset
@@ -260,7 +258,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     const float lg2_floor = (ALGO == CSE_ALGO_OMLSA) ? fast_log2(p2) : 0.0f;
     const float q_spp = fminf(fmaxf(p3, 1e-3f), 1.0f - 1e-3f);
 
-    // ---- pass-1 twiddles e^{2πi i b/M}, [b][i], shared by the workgroup
+    // ---- pass-1 twiddles e^{2πi i b/M}, [b-1][i], shared by the workgroup
     for (int e = tid; e < 15 * L; e += W::THREADS) {
         const int b = 1 + e / L, ii = e % L;
         double s, c;
@@ -268,10 +266,10 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         ((cf*)(smem + W::OFF_TW))[e] = cmk((float)c, (float)s);
     }
 
-    // ---- row staging: thread tid owns Y/N elements tid + k*THREADS and clean[tid]
+    // ---- row staging: thread tid owns Y/N elements tid + u*THREADS, clean tid + u*THREADS
     float2 py[W::YPT];
     float pn[W::YPT];
-    float pc = 0.0f;
+    float pc[W::CPT];
     auto load_rows = [&](int t) {  // issue loads of frame t's rows into registers
         if (t < nf) {
 #pragma unroll
@@ -279,13 +277,15 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 const int k = tid + u * W::THREADS;
                 if (k < B) {
                     py[u] = Ybase[t * B + k];
-                    if (nstride) pn[u] = Nbase[t * (int)nstride + k];
+                    if (nstride) pn[u] = Nbase[t * nstride + k];
                 }
             }
         }
-        if (tid < HOP) {
-            const int o = t * HOP - NFFT / 2 + tid;
-            pc = (cbase && o >= 0 && o < len) ? (float)cbase[o] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < W::CPT; ++u) {
+            const int j = tid + u * W::THREADS;
+            const int o = t * HOP - NFFT / 2 + j;
+            pc[u] = (j < HOP && cbase && o >= 0 && o < len) ? (float)cbase[o] : 0.0f;
         }
     };
     auto store_rows = [&](int t) {  // registers -> LDS rows of frame t
@@ -299,7 +299,11 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 }
             }
         }
-        if (tid < HOP) crow[(t & 1) * W::HMAX + tid] = pc;
+#pragma unroll
+        for (int u = 0; u < W::CPT; ++u) {
+            const int j = tid + u * W::THREADS;
+            if (j < HOP) crow[(t & 1) * W::HMAX + j] = pc[u];
+        }
     };
     if (!nstride) {  // static noise row: once
         for (int k = tid; k < B; k += W::THREADS) nrow[k] = Nbase[k];
@@ -336,48 +340,54 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     bool fin = true;
 
     for (int t = 0; t < nf + R - 1; ++t) {
-        // Keep the lane rotors opaque per frame: otherwise LICM hoists the 32
-        // window values and 16 packing twiddles derived from them out of the
-        // loop (64 live VGPRs, spills).  Recomputing them costs ~130 FMAs/frame.
+        // Keep lane rotors and LDS bases opaque per frame: otherwise LICM hoists
+        // the 32 window values, 16 packing twiddles and ~40 per-index LDS
+        // addresses derived from them into long-lived VGPRs (spills).
         asm volatile("" : "+v"(bc), "+v"(bs), "+v"(wc[0]), "+v"(wc[1]), "+v"(ws[0]),
                      "+v"(ws[1]), "+v"(pc2[0]), "+v"(pc2[1]), "+v"(ps2[0]), "+v"(ps2[1]));
         const cf base = cmk(bc, bs);
         if (t < nf) {
             __syncthreads();  // rows(t) visible; last frame's transpose reads done
             // ---------------- gain stage: S = Y * G into my cell's LDS row
+            {
+                cf* sb = (cf*)(smem + opaque(creg + 8 * i));   // &S[i]
+                const float2* yr = (const float2*)((unsigned char*)yrow + opaque(8 * i));
+                const float* nr = (const float*)((unsigned char*)nrow + opaque(4 * i));
 #pragma unroll
-            for (int j = 0; j < 17; ++j) {
-                if (j == 16 && i != 0) continue;
-                const int k = (j < 16) ? i + L * j : M;
-                const float2 y = yrow[k];
-                const float nz = nrow[k];
-                const float P = y.x * y.x + y.y * y.y;
-                float g;
-                cf Sj;
-                if (ALGO == CSE_ALGO_SS) {
-                    // Ps = max(P - a N, b N); |S| = sqrt(Ps) with the noisy phase
-                    // (spectral_subtractor.py:44-53).  No eps floor: the
-                    // reference floors BEFORE fix_length (engine.noise_key).
-                    const float ps = fmaxf(P - p0 * nz, p1 * nz);
-                    const float sp = __builtin_amdgcn_sqrtf(ps);
-                    if (P > 0.0f) {
-                        g = sp * __builtin_amdgcn_rsqf(P);
+                for (int j = 0; j < 17; ++j) {
+                    if (j == 16 && i != 0) continue;
+                    const int kk = (j < 16) ? L * j : M;  // k - i
+                    const float2 y = yr[kk];
+                    const float nz = nr[kk];
+                    const float P = y.x * y.x + y.y * y.y;
+                    float g;
+                    cf Sj;
+                    if (ALGO == CSE_ALGO_SS) {
+                        // Ps = max(P - a N, b N); |S| = sqrt(Ps) with the noisy phase
+                        // (spectral_subtractor.py:44-53).  No eps floor: the
+                        // reference floors BEFORE fix_length (engine.noise_key).
+                        const float ps = fmaxf(P - p0 * nz, p1 * nz);
+                        const float sp = __builtin_amdgcn_sqrtf(ps);
+                        if (P > 0.0f) {
+                            g = sp * __builtin_amdgcn_rsqf(P);
+                            Sj = cmk(y.x * g, y.y * g);
+                        } else {  // angle(0) = 0
+                            g = 0.0f;
+                            Sj = cmk(sp, 0.0f);
+                        }
+                    } else {
+                        if (ALGO == CSE_ALGO_WIENER)
+                            g = gain_wiener(P, nz, t == 0, rr[j], p0, p1);
+                        else if (ALGO == CSE_ALGO_MMSE)
+                            g = gain_mmse(P, nz, t == 0, rr[j], p0, p1, p2, p3);
+                        else
+                            g = gain_omlsa(P, nz, t == 0, rr[j], p0, p1, p2, lg2_floor, q_spp,
+                                           p4);
                         Sj = cmk(y.x * g, y.y * g);
-                    } else {  // angle(0) = 0
-                        g = 0.0f;
-                        Sj = cmk(sp, 0.0f);
                     }
-                } else {
-                    if (ALGO == CSE_ALGO_WIENER)
-                        g = gain_wiener(P, nz, t == 0, rr[j], p0, p1);
-                    else if (ALGO == CSE_ALGO_MMSE)
-                        g = gain_mmse(P, nz, t == 0, rr[j], p0, p1, p2, p3);
-                    else
-                        g = gain_omlsa(P, nz, t == 0, rr[j], p0, p1, p2, lg2_floor, q_spp, p4);
-                    Sj = cmk(y.x * g, y.y * g);
+                    sb[kk] = Sj;
+                    if (OUT && gout) gout[t * B + i + kk] = g;
                 }
-                sb[k] = Sj;
-                if (OUT && gout) gout[t * B + k] = g;
             }
             __syncthreads();  // S rows complete; every wave is done with yrow/nrow(t)
             store_rows(t + 1);
@@ -386,41 +396,53 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             // ---------------- pass 1: real-IFFT packing + DFT16 over j -----
             // Z'[k] = (X_k + X*_{M-k}) + i (X_k - X*_{M-k}) e^{2πi k/NFFT}
             cf z[16];
+            {
+                const cf* sa = (const cf*)(smem + opaque(creg + 8 * i));                   // S[i + L j]
+                const cf* sm = (const cf*)(smem + opaque(creg + 8 * (M - i - 15 * L)));   // S[M - i - L j]
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int k = i + L * j;
-                cf A = sb[k];
-                cf Bm = sb[M - k];
-                if (k == 0) {  // irfft ignores the imaginary parts of DC and Nyquist
-                    A.y = 0.0f;
-                    Bm.y = 0.0f;
+                for (int j = 0; j < 16; ++j) {
+                    cf A = sa[L * j];
+                    cf Bm = sm[L * (15 - j)];
+                    if (j == 0 && i == 0) {  // irfft ignores Im of DC and Nyquist
+                        A.y = 0.0f;
+                        Bm.y = 0.0f;
+                    }
+                    const cf Bc = cconj(Bm);
+                    const cf tw = cmul(base, cmk(Rot32::c[j], Rot32::s[j]));  // e^{2πi k/NFFT}
+                    z[j] = cadd(cadd(A, Bc), cmuli(cmul(csub(A, Bc), tw)));
                 }
-                const cf Bc = cconj(Bm);
-                const cf tw = cmul(base, cmk(Rot32::c[j], Rot32::s[j]));  // e^{2πi k/NFFT}
-                z[j] = cadd(cadd(A, Bc), cmuli(cmul(csub(A, Bc), tw)));
             }
             idft16(z);
+            {
+                const cf* tw = (const cf*)((const unsigned char*)tw1 + opaque(8 * i));
 #pragma unroll
-            for (int b = 1; b < 16; ++b) z[b] = cmul(z[b], tw1[(b - 1) * L + i]);
+                for (int b = 1; b < 16; ++b) z[b] = cmul(z[b], tw[(b - 1) * L]);
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();  // my wave's S reads done (in-order LDS)
+            {
+                cf* tw_ = (cf*)(smem + opaque(creg + 8 * i));   // V[b][i] at b*TR + i
 #pragma unroll
-            for (int b = 0; b < 16; ++b) tb[b * L + (i ^ tswz<L>(b))] = z[b];
+                for (int b = 0; b < 16; ++b) tw_[b * TR] = z[b];
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();  // transpose block complete
 
             // ---------------- pass 2: DFT over the lane index --------------
             cf v[16];
-            if (L == 16) {
+            {
+                const cf* tr = (const cf*)(smem + opaque(creg + 8 * TR * b2));   // row V[b2][.]
+                if (L == 16) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] = tb[i * L + (r ^ tswz<L>(i))];
-            } else {  // DFT32 = butterfly (lo +- hi) * W32^{r h}, then DFT16
+                    for (int r = 0; r < 16; ++r) v[r] = tr[r];
+                } else {  // DFT32 = butterfly (lo +- hi) * W32^{r h}, then DFT16
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const cf lo = tb[b2 * L + (r ^ tswz<L>(b2))];
-                    const cf hi = tb[b2 * L + ((r + 16) ^ tswz<L>(b2))];
-                    const cf u = h2 ? csub(lo, hi) : cadd(lo, hi);
-                    v[r] = h2 ? cmul(u, cmk(Rot32::c[r], Rot32::s[r])) : u;
+                    for (int r = 0; r < 16; ++r) {
+                        const cf lo = tr[r];
+                        const cf hi = tr[r + 16];
+                        const cf u = h2 ? csub(lo, hi) : cadd(lo, hi);
+                        v[r] = h2 ? cmul(u, cmk(Rot32::c[r], Rot32::s[r])) : u;
+                    }
                 }
             }
             idft16(v);
@@ -442,52 +464,51 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         // y = ola / wss (librosa istft normalisation), then the SNR error sum
         // of the clipped sample (evaluation_metrics.py:52-56).  Steady frames
         // use the closed-form wss; the first R-1 and the flush frames sum the
-        // covering windows explicitly.
-        const float* crow_t = crow + (t & 1) * W::HMAX;
-        float inv_w[F];
-        if ((t < R - 1) || (t >= nf)) {
-#pragma unroll
-            for (int q = 0; q < F; ++q) {
-                float wss = 0.0f;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int tr = t - r;
-                    if (tr >= 0 && tr < nf) {
-                        const float w = hann_at<NFFT>((q >> 1) + r * (HOP / SP), q & 1, wc, ws) * NFFT;
-                        wss = fmaf(w, w, wss);
-                    }
-                }
-                inv_w[q] = wss > 0.0f ? __builtin_amdgcn_rcpf(wss) : 1.0f;
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < F; ++q) {
-                if (R == 2) {
-                    // 0.75 + 0.25 cos(2π n/256) for 512/256; n = 32 aq + off + e
-                    const int m = (4 * (q >> 1)) & 31;  // 2π(32 aq)/256 = 2π(4 aq)/32
-                    inv_w[q] = __builtin_amdgcn_rcpf(
-                        0.75f + 0.25f * (Rot32::c[m] * pc2[q & 1] - Rot32::s[m] * ps2[q & 1]));
-                } else {
-                    inv_w[q] = (R == 4) ? (1.0f / 1.5f) : (1.0f / 3.0f);
-                }
-            }
-        }
-        if (valid) {
+        // covering windows explicitly (a separate path, so its registers do
+        // not add to the steady loop's).
+        auto retire = [&](auto inv_of_q) {
+            if (!valid) return;
             const int o0 = t * HOP + off - NFFT / 2;  // output index of q = 0
+            const float* crow_t = (const float*)((const unsigned char*)crow +
+                                                 opaque(4 * ((t & 1) * W::HMAX + off)));
             float part = 0.0f;
 #pragma unroll
             for (int q = 0; q < F; ++q) {
                 const int n = SP * (q >> 1) + (q & 1);  // + off: position inside frame t
                 const int o = o0 + n;
                 if (o >= 0 && o < len) {
-                    const float y = acc[q] * inv_w[q];
+                    const float y = acc[q] * inv_of_q(q);
                     fin = fin && __builtin_isfinite(y);
                     if (OUT && yout) yout[o] = y;
-                    const float d = crow_t[n + off] - fminf(fmaxf(y, -1.0f), 1.0f);
+                    const float d = crow_t[n] - fminf(fmaxf(y, -1.0f), 1.0f);
                     part = fmaf(d, d, part);
                 }
             }
             sse += (double)part;
+        };
+        if ((t < R - 1) || (t >= nf)) {
+            retire([&](int q) {
+                float wss = 0.0f;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int tr = t - r;
+                    if (tr >= 0 && tr < nf) {
+                        const float w =
+                            hann_at<NFFT>((q >> 1) + r * (HOP / SP), q & 1, wc, ws) * NFFT;
+                        wss = fmaf(w, w, wss);
+                    }
+                }
+                return wss > 0.0f ? __builtin_amdgcn_rcpf(wss) : 1.0f;
+            });
+        } else if (R == 2) {
+            // 0.75 + 0.25 cos(2π n/256) for 512/256; n = 32 aq + off + e
+            retire([&](int q) {
+                const int m = (4 * (q >> 1)) & 31;  // 2π(32 aq)/256 = 2π(4 aq)/32
+                return __builtin_amdgcn_rcpf(
+                    0.75f + 0.25f * (Rot32::c[m] * pc2[q & 1] - Rot32::s[m] * ps2[q & 1]));
+            });
+        } else {
+            retire([&](int) { return (R == 4) ? (1.0f / 1.5f) : (1.0f / 3.0f); });
         }
 #pragma unroll
         for (int q = 0; q < 32 - F; ++q) acc[q] = acc[q + F];
@@ -522,7 +543,7 @@ __device__ __forceinline__ void dispatch_algo(const Args& a, const cse_cell_t* w
 // OUT: the y_out / g_out variant (parity tests, single-cell plugin calls);
 // the grid/bench path computes only the per-cell score sums.
 template <int NFFT, bool OUT>
-__global__ void __launch_bounds__(256, CSE_WAVES_PER_SIMD) enhance_kernel(Args a) {
+__global__ void __launch_bounds__(WG<NFFT>::THREADS, CSE_WAVES_PER_SIMD) enhance_kernel(Args a) {
     using W = WG<NFFT>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -569,20 +590,22 @@ extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells
     CSE_CHECK_ARG(groups < (1ll << 31), "cse_enhance_cells: too many cells");
     const bool out = (y_out != nullptr) || (g_out != nullptr);
     const void* fn;
-    int bytes;
+    int bytes, threads;
     if (n_fft == 512) {
         fn = out ? (const void*)enhance_kernel<512, true> : (const void*)enhance_kernel<512, false>;
         bytes = WG<512>::BYTES;
+        threads = WG<512>::THREADS;
     } else {
         fn = out ? (const void*)enhance_kernel<1024, true> : (const void*)enhance_kernel<1024, false>;
         bytes = WG<1024>::BYTES;
+        threads = WG<1024>::THREADS;
     }
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) {
         ::cse::set_error("cse_enhance_cells: cannot reserve %d bytes of LDS", bytes);
         return CSE_ELAUNCH;
     }
     void* args[] = {&a};
-    if (hipLaunchKernel(fn, dim3((unsigned)groups), dim3(256), args, (size_t)bytes,
+    if (hipLaunchKernel(fn, dim3((unsigned)groups), dim3(threads), args, (size_t)bytes,
                         (hipStream_t)stream) != hipSuccess) {
         ::cse::set_error("cse_enhance_cells: launch failed");
         return CSE_ELAUNCH;

@@ -214,6 +214,12 @@ __global__ void smooth_kernel(const float* __restrict__ N, int T, int B, int src
     }
 }
 
+__global__ void invert_kernel(const float* __restrict__ N, int64_t n, double eps,
+                              float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (float)(1.0 / fmax((double)N[i], eps));
+}
+
 struct Workspace {
     double* energy;  // [n_sig][T]
     int* sel;        // [n_sig][T]
@@ -335,5 +341,15 @@ extern "C" int cse_noise_smooth(const float* N, int64_t n_sig, int T, int B, int
     hipLaunchKernelGGL(smooth_kernel, dim3(ceil_div(B, 64), (unsigned)n_sig), dim3(64), 0,
                        (hipStream_t)stream, N, T, B, src_frames, m, out);
     CSE_CHECK_LAUNCH("cse_noise_smooth");
+    return CSE_OK;
+}
+
+extern "C" int cse_noise_invert(const float* N, int64_t n, double eps, float* out,
+                                cse_stream_t stream) {
+    CSE_CHECK_ARG(N && out && n >= 0 && eps > 0.0, "cse_noise_invert: bad arguments");
+    if (n == 0) return CSE_OK;
+    hipLaunchKernelGGL(invert_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, N,
+                       n, eps, out);
+    CSE_CHECK_LAUNCH("cse_noise_invert");
     return CSE_OK;
 }

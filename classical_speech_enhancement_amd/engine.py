@@ -57,7 +57,7 @@ def n_frames(length, hop):
 def noise_key(alg, params, T):
     """Which noise PSD array a cell reads, mirroring each algorithm's pipeline.
 
-    Returns (method, pct, eps, expand, mu):
+    Returns (method, pct, eps, expand, mu, inverse):
       - every algorithm estimates with the eps it passes (ss/wiener/omlsa 1e-10,
         mmse 1e-12: spectral_subtractor.py:17, wiener_filter.py:23, mmse.py:17,
         advanced_mmse.py:26);
@@ -69,7 +69,9 @@ def noise_key(alg, params, T):
         the estimate, later frames see 0 (SS) or, after OMLSA's smoothing,
         mu**t times it;
       - mmse/omlsa smooth any time-varying estimate except true_noise
-        (mmse.py:48-54, advanced_mmse.py:60-66); mu=None means no smoothing.
+        (mmse.py:48-54, advanced_mmse.py:60-66); mu=None means no smoothing;
+      - inverse: Wiener/MMSE/OMLSA read 1/max(N, eps) (their in-loop floor,
+        wiener_filter.py:122, mmse.py:71, advanced_mmse.py:207), SS reads N.
     A key is static (one [B] row for all frames) iff expand is False and the
     method is percentile/simple.
     """
@@ -91,11 +93,11 @@ def noise_key(alg, params, T):
             mu = float(params.get("noise_mu", 0.98))
         elif code == "OMLSA":
             mu = float(params["noise_mu"])
-    return (method, pct, eps, expand, mu)
+    return (method, pct, eps, expand, mu, code != "SS")
 
 
 def key_is_static(key):
-    method, _, _, expand, mu = key
+    method, _, _, expand, mu, _ = key
     return method in ("percentile", "simple") and not expand and mu is None
 
 
@@ -210,15 +212,16 @@ class GridPlan:
             per_sig = B if static else T * B
             self.pool_off[(hop, key)] = (noff, 0 if static else B, per_sig)
             noff += S * per_sig
-            method, _, _, expand, mu = key
+            method, _, _, expand, mu, inverse = key
             if method == "true_noise" and hop not in self.Ptrue:
                 if not with_clean:
                     raise ValueError("TrueNoiseEstimator requires clean_audio and noisy_audio")
                 self.Ptrue[hop] = torch.empty((S, T, B), dtype=torch.float64, device=dev)
-            if expand or mu is not None:  # estimate into scratch, then smooth into the pool
+            if expand or mu is not None or inverse:  # chain through scratch buffers
                 tmp_need = max(tmp_need, S * T * B)
         self.pool = torch.empty(noff, dtype=torch.float32, device=dev)
         self.scratch = torch.empty(max(tmp_need, 1), dtype=torch.float32, device=dev)
+        self.scratch2 = torch.empty(max(tmp_need, 1), dtype=torch.float32, device=dev)
         Tmax = max(n_frames(L, h) for h in self.hops)
         self.ws = torch.empty(int(eng.lib.cse_noise_workspace_bytes(S, Tmax, B)),
                               dtype=torch.uint8, device=dev)
@@ -277,22 +280,29 @@ class GridPlan:
                 _lib.check(lib.cse_stft(_ptr(noisy), _ptr(clean), S, L, self.n_fft, hop, None,
                                         _ptr(self.Ptrue[hop]), _stream()), "cse_stft(true)")
         for (hop, key) in self.keys:
-            method, pct, eps, expand, mu = key
+            method, pct, eps, expand, mu, inverse = key
             T = n_frames(L, hop)
             o, stride, per_sig = self.pool_off[(hop, key)]
             dst = self.pool[o:o + S * per_sig]
             smooth = expand or mu is not None
-            tgt = self.scratch if smooth else dst
+            # estimate -> [smooth] -> [invert]; the last step writes the pool slice
+            est_out = dst if not (smooth or inverse) else self.scratch
             if method == "true_noise":
-                self._est("true_noise", self.Ptrue[hop], 0.0, eps, tgt)
+                self._est("true_noise", self.Ptrue[hop], 0.0, eps, est_out)
             elif method == "simple":
-                self._est("percentile", self.P[hop], 25.0, eps, tgt)
+                self._est("percentile", self.P[hop], 25.0, eps, est_out)
             else:
-                self._est(method, self.P[hop], pct if pct is not None else 20.0, eps, tgt)
+                self._est(method, self.P[hop], pct if pct is not None else 20.0, eps, est_out)
+            cur = est_out
             if smooth:
+                sm_out = dst if not inverse else self.scratch2
                 src_frames = 1 if method in ("percentile", "simple") else T
-                _lib.check(lib.cse_noise_smooth(_ptr(tgt), S, T, B, src_frames, float(mu or 0.0),
-                                                _ptr(dst), _stream()), "cse_noise_smooth")
+                _lib.check(lib.cse_noise_smooth(_ptr(cur), S, T, B, src_frames, float(mu or 0.0),
+                                                _ptr(sm_out), _stream()), "cse_noise_smooth")
+                cur = sm_out
+            if inverse:
+                _lib.check(lib.cse_noise_invert(_ptr(cur), S * per_sig, float(eps), _ptr(dst),
+                                                _stream()), "cse_noise_invert")
         self.clean = clean if self.with_clean else None
 
     def enhance(self):

@@ -60,8 +60,8 @@ enum {
 
 /*
  * One grid cell = one (signal group, noise PSD, algorithm, parameter set).
- * Cells are processed CSE_CELLS_PER_GROUP(n_fft) at a time by one 256-thread
- * workgroup (4 wavefronts) that stages their shared rows in LDS, so the cells
+ * Cells are processed CSE_CELLS_PER_GROUP(n_fft) at a time by one 192-thread
+ * workgroup (3 wavefronts) that stages their shared rows in LDS, so the cells
  * of one such slot group (cells[g*G .. g*G+G-1]) MUST share algo, hop,
  * y_offset, noise_offset, noise_stride and clean_offset; pad a short group
  * with CSE_ALGO_NONE slots.  Only param, out_offset and gain_offset may differ.
@@ -70,7 +70,8 @@ typedef struct cse_cell {
     int32_t algo;          /* CSE_ALGO_* */
     int32_t hop;           /* hop length; 128 or 256 */
     int64_t y_offset;      /* offset (in complex elements) of this cell's spectrum Y[T][B] */
-    int64_t noise_offset;  /* offset (floats) of this cell's noise PSD */
+    int64_t noise_offset;  /* offset (floats) of this cell's noise row: the PSD N itself for
+                              CSE_ALGO_SS, 1/max(N, eps) (cse_noise_invert) for the others */
     int64_t noise_stride;  /* floats between frames of the noise PSD: 0 = static [B], B = [T][B] */
     int64_t clean_offset;  /* offset (doubles) of the clean reference for the SNR, or -1 */
     int64_t out_offset;    /* offset (floats) of this cell's output waveform in y_out, or -1 */
@@ -78,7 +79,7 @@ typedef struct cse_cell {
     float param[8];        /* algorithm parameters, order as in the CSE_ALGO_* comments */
 } cse_cell_t;              /* 88 bytes */
 
-#define CSE_CELLS_PER_GROUP(n_fft) ((n_fft) == 512 ? 16 : 8)
+#define CSE_CELLS_PER_GROUP(n_fft) ((n_fft) == 512 ? 12 : 6)
 
 /* Library identity. */
 int cse_version(void);
@@ -124,6 +125,13 @@ int cse_noise_estimate(int method, const double* P, int64_t n_sig, int T, int B,
  */
 int cse_noise_smooth(const float* N, int64_t n_sig, int T, int B, int src_frames, double mu,
                      float* out, cse_stream_t stream);
+
+/*
+ * out = 1 / max(N, eps) (fp64 math, f32 out), n elements: the noise row the
+ * Wiener/MMSE/OMLSA cells of cse_enhance_cells read (their in-loop floors,
+ * wiener_filter.py:122, mmse.py:71, advanced_mmse.py:207, folded in).
+ */
+int cse_noise_invert(const float* N, int64_t n, double eps, float* out, cse_stream_t stream);
 
 /*
  * 1 / window-sum-square of the ISTFT (librosa 0.11 istft normalisation) for a

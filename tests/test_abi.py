@@ -66,10 +66,11 @@ def test_wave_packing_groups_and_pads():
     cells["hop"] = [128, 128, 256, 128, 128, 128, 128]
     cells["y_offset"] = [0, 0, 5, 0, 0, 0, 0]
     packed, order = pack_waves(cells, 512)
-    assert len(packed) % 16 == 0
+    G = _lib.cells_per_group(512)
+    assert len(packed) % G == 0
     assert sorted(order[order >= 0].tolist()) == list(range(7))
-    for w in range(len(packed) // 16):
-        slots = packed[16 * w:16 * w + 16]
+    for w in range(len(packed) // G):
+        slots = packed[G * w:G * w + G]
         real = slots[slots["algo"] >= 0]
         for f in ("hop", "algo", "y_offset", "noise_offset", "noise_stride", "clean_offset"):
             assert len(set(slots[f].tolist() if f != "algo" else real[f].tolist())) == 1, f
