@@ -24,9 +24,16 @@ CELL_DTYPE = np.dtype([
 ], align=True)
 assert CELL_DTYPE.itemsize == 88
 
+# numpy mirror of cse_noise_job_t — 40 bytes
+NOISE_JOB_DTYPE = np.dtype([
+    ("src_offset", np.int64), ("dst_offset", np.int64), ("src_frames", np.int32),
+    ("out_frames", np.int32), ("mu", np.float64), ("inv_eps", np.float64)], align=True)
+assert NOISE_JOB_DTYPE.itemsize == 40
+
 EXPORTS = ("cse_version", "cse_last_error", "cse_stft", "cse_noise_workspace_bytes",
-           "cse_noise_estimate", "cse_noise_smooth", "cse_noise_invert", "cse_istft_norm",
-           "cse_enhance_cells")
+           "cse_noise_estimate", "cse_noise_smooth", "cse_noise_median",
+           "cse_noise_percentile_med", "cse_noise_min_tracking_med", "cse_noise_finish",
+           "cse_noise_invert", "cse_istft_norm", "cse_enhance_cells")
 
 
 def cells_per_group(n_fft):
@@ -63,6 +70,14 @@ def load(path=LIB_PATH):
     lib.cse_noise_estimate.argtypes = [i32, P, i64, i32, i32, f64, f64, P, P, P]
     lib.cse_noise_smooth.restype = i32
     lib.cse_noise_smooth.argtypes = [P, i64, i32, i32, i32, f64, P, P]
+    lib.cse_noise_median.restype = i32
+    lib.cse_noise_median.argtypes = [P, i64, i32, i32, P, P]
+    lib.cse_noise_percentile_med.restype = i32
+    lib.cse_noise_percentile_med.argtypes = [P, P, i64, i32, i32, f64, f64, P, P, P]
+    lib.cse_noise_min_tracking_med.restype = i32
+    lib.cse_noise_min_tracking_med.argtypes = [P, P, i64, i32, i32, f64, P, f64, P, P, P]
+    lib.cse_noise_finish.restype = i32
+    lib.cse_noise_finish.argtypes = [P, i32, i64, i32, P, P, P]
     lib.cse_noise_invert.restype = i32
     lib.cse_noise_invert.argtypes = [P, i64, f64, P, P]
     lib.cse_istft_norm.restype = i32

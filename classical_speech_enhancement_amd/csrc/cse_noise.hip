@@ -125,7 +125,9 @@ __global__ void bin_stats_kernel(const double* __restrict__ P, int T, int B, int
     const int64_t sig = blockIdx.y;
     const double* Ps = P + sig * (int64_t)T * B + b;
     double median = 0.0;
-    if (mode != STATS_SIMPLE) {
+    if (mode == STATS_PERCENTILE && med) {
+        median = med[sig * B + b];  // precomputed by cse_noise_median
+    } else if (mode != STATS_SIMPLE) {
         for (int i = threadIdx.x; i < n2_all; i += blockDim.x)
             s[i] = i < T ? Ps[(int64_t)i * B] : INFINITY;
         __syncthreads();
@@ -168,7 +170,18 @@ __global__ void iir_kernel(const double* __restrict__ P, int T, int B, double a,
     double s = Ps[0];
     Ss[0] = s;
     const double c = 1.0 - a;
-    for (int t = 1; t < T; ++t) {
+    int t = 1;
+    for (; t + 8 <= T; t += 8) {  // loads first: the recurrence is the only dependency
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = Ps[(int64_t)(t + u) * B];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            s = __dadd_rn(__dmul_rn(a, s), __dmul_rn(c, x[u]));
+            Ss[(int64_t)(t + u) * B] = s;
+        }
+    }
+    for (; t < T; ++t) {
         s = __dadd_rn(__dmul_rn(a, s), __dmul_rn(c, Ps[(int64_t)t * B]));
         Ss[(int64_t)t * B] = s;
     }
@@ -177,7 +190,7 @@ __global__ void iir_kernel(const double* __restrict__ P, int T, int B, double a,
 // minimum_filter1d(S, size=w, mode='nearest') then floors (noise_estimation.py:86-95)
 __global__ void min_filter_kernel(const double* __restrict__ S, int T, int B, int half,
                                   const double* __restrict__ med, double eps,
-                                  float* __restrict__ N) {
+                                  float* __restrict__ N, double eps_b, float* __restrict__ Nb) {
     const int t = blockIdx.x;
     const int64_t sig = blockIdx.y;
     const int lo = t - half < 0 ? 0 : t - half;
@@ -186,8 +199,9 @@ __global__ void min_filter_kernel(const double* __restrict__ S, int T, int B, in
         const double* Ss = S + sig * (int64_t)T * B + b;
         double m = Ss[(int64_t)lo * B];
         for (int u = lo + 1; u <= hi; ++u) m = fmin(m, Ss[(int64_t)u * B]);
-        const double v = fmax(fmax(m, 0.01 * med[sig * B + b]), eps);
-        N[(sig * T + t) * (int64_t)B + b] = (float)v;
+        const double f = fmax(m, 0.01 * med[sig * B + b]);
+        N[(sig * T + t) * (int64_t)B + b] = (float)fmax(f, eps);
+        if (Nb) Nb[(sig * T + t) * (int64_t)B + b] = (float)fmax(f, eps_b);
     }
 }
 
@@ -218,6 +232,41 @@ __global__ void invert_kernel(const float* __restrict__ N, int64_t n, double eps
                               float* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = (float)(1.0 / fmax((double)N[i], eps));
+}
+
+// batched post-processing of noise rows: smoothing over frames, zero-padding a
+// static row to out_frames (librosa fix_length), optional 1/max(., eps)
+__global__ void finish_kernel(const cse_noise_job_t* __restrict__ jobs, int B,
+                              const float* __restrict__ src, float* __restrict__ dst) {
+    const cse_noise_job_t jb = jobs[blockIdx.z];
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t sig = blockIdx.y;
+    if (b >= B) return;
+    const float* Ns = src + jb.src_offset + sig * (int64_t)jb.src_frames * B + b;
+    float* Os = dst + jb.dst_offset + sig * (int64_t)jb.out_frames * B + b;
+    const double mu = jb.mu, c = 1.0 - mu, ie = jb.inv_eps;
+    auto put = [&](int t, double v) {
+        Os[(int64_t)t * B] = ie > 0.0 ? (float)(1.0 / fmax(v, ie)) : (float)v;
+    };
+    double s = (double)Ns[0];
+    put(0, s);
+    int t = 1;
+    for (; t + 8 <= jb.out_frames; t += 8) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            x[u] = (t + u) < jb.src_frames ? (double)Ns[(int64_t)(t + u) * B] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            s = __dadd_rn(__dmul_rn(mu, s), __dmul_rn(c, x[u]));
+            put(t + u, s);
+        }
+    }
+    for (; t < jb.out_frames; ++t) {
+        const double x = t < jb.src_frames ? (double)Ns[(int64_t)t * B] : 0.0;
+        s = __dadd_rn(__dmul_rn(mu, s), __dmul_rn(c, x));
+        put(t, s);
+    }
 }
 
 struct Workspace {
@@ -262,9 +311,85 @@ static void quiet_count(int T, double pct_in, int* k_out, double* pct_out) {
     *pct_out = pct;
 }
 
+static int launch_median(const double* P, int64_t n_sig, int T, int B, double* med,
+                         hipStream_t s) {
+    const int n2_all = next_pow2(T);
+    hipLaunchKernelGGL(bin_stats_kernel, dim3(B, (unsigned)n_sig), dim3(256),
+                       (size_t)n2_all * sizeof(double), s, P, T, B, n2_all, (int)STATS_MEDIAN,
+                       (const int*)nullptr, 0, 0, 0.0, 0.0, 0.0, med, (float*)nullptr, 0);
+    CSE_CHECK_LAUNCH("noise median");
+    return CSE_OK;
+}
+
+static int launch_simple(const double* P, int64_t n_sig, int T, int B, double eps, float* N,
+                         int broadcast, hipStream_t s) {
+    const int n2_all = next_pow2(T);
+    hipLaunchKernelGGL(bin_stats_kernel, dim3(B, (unsigned)n_sig), dim3(256),
+                       (size_t)n2_all * sizeof(double), s, P, T, B, n2_all, (int)STATS_SIMPLE,
+                       (const int*)nullptr, 0, 0, 0.0, 0.0, eps, (double*)nullptr, N, broadcast);
+    CSE_CHECK_LAUNCH("noise simple");
+    return CSE_OK;
+}
+
+static int launch_percentile(const double* P, const double* med, int64_t n_sig, int T, int B,
+                             double percentile, double eps, float* N, Workspace w,
+                             hipStream_t s) {
+    int k;
+    double pct;
+    quiet_count(T, percentile, &k, &pct);
+    const int n2_all = next_pow2(T), n2_sel = next_pow2(k);
+    hipLaunchKernelGGL(frame_energy_kernel, dim3(T, (unsigned)n_sig), dim3(256), 0, s, P, T, B,
+                       eps, w.energy);
+    hipLaunchKernelGGL(select_quiet_kernel, dim3((unsigned)n_sig), dim3(1024),
+                       (size_t)n2_all * 12, s, (const double*)w.energy, T, n2_all, k, w.sel);
+    hipLaunchKernelGGL(bin_stats_kernel, dim3(B, (unsigned)n_sig), dim3(256),
+                       (size_t)n2_sel * sizeof(double), s, P, T, B, n2_all,
+                       (int)STATS_PERCENTILE, (const int*)w.sel, k, n2_sel, pct / 100.0, 0.02,
+                       eps, (double*)med, N, 0);
+    CSE_CHECK_LAUNCH("noise percentile");
+    return CSE_OK;
+}
+
+static int launch_min_tracking(const double* P, const double* med, int64_t n_sig, int T, int B,
+                               double eps, float* N, double eps_b, float* Nb, Workspace w,
+                               hipStream_t s) {
+    const double a = fmax(0.8, fmin(0.95, 1.0 - 5.0 / (double)T));
+    int win = T < 50 ? T : 50;  // min(max(3, 50), T), made odd
+    if (win % 2 == 0) win += 1;
+    hipLaunchKernelGGL(iir_kernel, dim3(ceil_div(B, 64), (unsigned)n_sig), dim3(64), 0, s, P, T, B,
+                       a, w.S);
+    hipLaunchKernelGGL(min_filter_kernel, dim3(T, (unsigned)n_sig), dim3(256), 0, s,
+                       (const double*)w.S, T, B, win / 2, med, eps, N, eps_b, Nb);
+    CSE_CHECK_LAUNCH("noise min tracking");
+    return CSE_OK;
+}
+
+static bool lds_ready = false;
+static int reserve_lds() {
+    if (!lds_ready) {
+        if (hipFuncSetAttribute((const void*)select_quiet_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kMaxSortFrames * 12) != hipSuccess ||
+            hipFuncSetAttribute((const void*)bin_stats_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kMaxSortFrames * 8) != hipSuccess) {
+            ::cse::set_error("noise kernels: cannot reserve LDS");
+            return CSE_ELAUNCH;
+        }
+        lds_ready = true;
+    }
+    return CSE_OK;
+}
+
 }  // namespace cse
 
 using namespace cse;
+
+#define CSE_NOISE_SHAPE_CHECKS(fn)                                                            \
+    CSE_CHECK_ARG(P != nullptr, fn ": P is NULL");                                            \
+    CSE_CHECK_ARG(n_sig > 0 && n_sig < 65536 && T >= 1 && B >= 2,                             \
+                  fn ": bad shape n_sig=%lld T=%d B=%d", (long long)n_sig, T, B);             \
+    CSE_CHECK_ARG(T <= kMaxSortFrames, fn ": T=%d > %d frames unsupported", T, kMaxSortFrames)
 
 extern "C" int64_t cse_noise_workspace_bytes(int64_t n_sig, int T, int B) {
     return align256(n_sig * (int64_t)T * 8) + align256(n_sig * (int64_t)T * 4) +
@@ -275,11 +400,8 @@ extern "C" int cse_noise_estimate(int method, const double* P, int64_t n_sig, in
                                   double percentile, double eps, float* N, void* workspace,
                                   cse_stream_t stream) {
     hipStream_t s = (hipStream_t)stream;
-    CSE_CHECK_ARG(P && N, "cse_noise_estimate: NULL P or N");
-    CSE_CHECK_ARG(n_sig > 0 && n_sig < 65536 && T >= 1 && B >= 2,
-                  "cse_noise_estimate: bad shape n_sig=%lld T=%d B=%d", (long long)n_sig, T, B);
-    CSE_CHECK_ARG(T <= kMaxSortFrames, "cse_noise_estimate: T=%d > %d frames unsupported", T,
-                  kMaxSortFrames);
+    CSE_NOISE_SHAPE_CHECKS("cse_noise_estimate");
+    CSE_CHECK_ARG(N != nullptr, "cse_noise_estimate: N is NULL");
     if (method == CSE_NOISE_TRUE) {
         const int64_t n = n_sig * (int64_t)T * B;
         hipLaunchKernelGGL(floor_cast_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, s, P, n, eps,
@@ -290,44 +412,58 @@ extern "C" int cse_noise_estimate(int method, const double* P, int64_t n_sig, in
     CSE_CHECK_ARG(method == CSE_NOISE_PERCENTILE || method == CSE_NOISE_MIN_TRACKING,
                   "Unbekannte Methode: %d", method);
     CSE_CHECK_ARG(workspace != nullptr, "cse_noise_estimate: workspace is NULL");
+    int rc = reserve_lds();
+    if (rc) return rc;
     Workspace w = carve(workspace, n_sig, T, B);
-    const int n2_all = next_pow2(T);
-    const size_t lds_all = (size_t)n2_all * sizeof(double);
-    dim3 grid_bins(B, (unsigned)n_sig);
-    if (T < 5) {  // noise_estimation.py:194-195
-        hipLaunchKernelGGL(bin_stats_kernel, grid_bins, dim3(256), lds_all, s, P, T, B, n2_all,
-                           (int)STATS_SIMPLE, (const int*)nullptr, 0, 0, 0.0, 0.0, eps,
-                           (double*)nullptr, N, method == CSE_NOISE_MIN_TRACKING ? 1 : 0);
-        CSE_CHECK_LAUNCH("cse_noise_estimate(simple)");
-        return CSE_OK;
-    }
-    if (method == CSE_NOISE_PERCENTILE) {
-        int k;
-        double pct;
-        quiet_count(T, percentile, &k, &pct);
-        const int n2_sel = next_pow2(k);
-        hipLaunchKernelGGL(frame_energy_kernel, dim3(T, (unsigned)n_sig), dim3(256), 0, s, P, T,
-                           B, eps, w.energy);
-        hipLaunchKernelGGL(select_quiet_kernel, dim3((unsigned)n_sig), dim3(1024),
-                           (size_t)n2_all * 12, s, (const double*)w.energy, T, n2_all, k, w.sel);
-        hipLaunchKernelGGL(bin_stats_kernel, grid_bins, dim3(256), lds_all, s, P, T, B, n2_all,
-                           (int)STATS_PERCENTILE, (const int*)w.sel, k, n2_sel, pct / 100.0,
-                           0.02, eps, w.med, N, 0);
-        CSE_CHECK_LAUNCH("cse_noise_estimate(percentile)");
-        return CSE_OK;
-    }
-    // min tracking
-    const double a = fmax(0.8, fmin(0.95, 1.0 - 5.0 / (double)T));
-    int win = T < 50 ? T : 50;  // min(max(3, 50), T)
-    if (win % 2 == 0) win += 1;
-    hipLaunchKernelGGL(bin_stats_kernel, grid_bins, dim3(256), lds_all, s, P, T, B, n2_all,
-                       (int)STATS_MEDIAN, (const int*)nullptr, 0, 0, 0.0, 0.0, eps, w.med,
-                       (float*)nullptr, 0);
-    hipLaunchKernelGGL(iir_kernel, dim3(ceil_div(B, 64), (unsigned)n_sig), dim3(64), 0, s, P, T, B,
-                       a, w.S);
-    hipLaunchKernelGGL(min_filter_kernel, dim3(T, (unsigned)n_sig), dim3(256), 0, s,
-                       (const double*)w.S, T, B, win / 2, (const double*)w.med, eps, N);
-    CSE_CHECK_LAUNCH("cse_noise_estimate(min_tracking)");
+    if (T < 5)  // noise_estimation.py:194-195
+        return launch_simple(P, n_sig, T, B, eps, N, method == CSE_NOISE_MIN_TRACKING, s);
+    rc = launch_median(P, n_sig, T, B, w.med, s);
+    if (rc) return rc;
+    if (method == CSE_NOISE_PERCENTILE)
+        return launch_percentile(P, w.med, n_sig, T, B, percentile, eps, N, w, s);
+    return launch_min_tracking(P, w.med, n_sig, T, B, eps, N, 0.0, nullptr, w, s);
+}
+
+extern "C" int cse_noise_median(const double* P, int64_t n_sig, int T, int B, double* med,
+                                cse_stream_t stream) {
+    CSE_NOISE_SHAPE_CHECKS("cse_noise_median");
+    CSE_CHECK_ARG(med != nullptr, "cse_noise_median: med is NULL");
+    int rc = reserve_lds();
+    if (rc) return rc;
+    return launch_median(P, n_sig, T, B, med, (hipStream_t)stream);
+}
+
+extern "C" int cse_noise_percentile_med(const double* P, const double* med, int64_t n_sig, int T,
+                                        int B, double percentile, double eps, float* N,
+                                        void* workspace, cse_stream_t stream) {
+    CSE_NOISE_SHAPE_CHECKS("cse_noise_percentile_med");
+    CSE_CHECK_ARG(med && N && workspace, "cse_noise_percentile_med: NULL pointer");
+    CSE_CHECK_ARG(T >= 5, "cse_noise_percentile_med: T=%d < 5 (use the simple estimate)", T);
+    int rc = reserve_lds();
+    if (rc) return rc;
+    return launch_percentile(P, med, n_sig, T, B, percentile, eps, N,
+                             carve(workspace, n_sig, T, B), (hipStream_t)stream);
+}
+
+extern "C" int cse_noise_min_tracking_med(const double* P, const double* med, int64_t n_sig,
+                                          int T, int B, double eps, float* N, double eps_b,
+                                          float* N_b, void* workspace, cse_stream_t stream) {
+    CSE_NOISE_SHAPE_CHECKS("cse_noise_min_tracking_med");
+    CSE_CHECK_ARG(med && N && workspace, "cse_noise_min_tracking_med: NULL pointer");
+    CSE_CHECK_ARG(T >= 5, "cse_noise_min_tracking_med: T=%d < 5 (use the simple estimate)", T);
+    return launch_min_tracking(P, med, n_sig, T, B, eps, N, eps_b, N_b,
+                               carve(workspace, n_sig, T, B), (hipStream_t)stream);
+}
+
+extern "C" int cse_noise_finish(const cse_noise_job_t* jobs, int n_jobs, int64_t n_sig, int B,
+                                const float* src, float* dst, cse_stream_t stream) {
+    CSE_CHECK_ARG(jobs && src && dst && n_jobs >= 0 && n_jobs < 65536,
+                  "cse_noise_finish: bad arguments");
+    CSE_CHECK_ARG(n_sig > 0 && n_sig < 65536 && B >= 1, "cse_noise_finish: bad shape");
+    if (n_jobs == 0) return CSE_OK;
+    hipLaunchKernelGGL(finish_kernel, dim3(ceil_div(B, 64), (unsigned)n_sig, (unsigned)n_jobs),
+                       dim3(64), 0, (hipStream_t)stream, jobs, B, src, dst);
+    CSE_CHECK_LAUNCH("cse_noise_finish");
     return CSE_OK;
 }
 

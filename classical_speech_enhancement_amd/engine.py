@@ -199,29 +199,44 @@ class GridPlan:
         self.P = {h: torch.empty((S, n_frames(L, h), B), dtype=torch.float64, device=dev)
                   for h in self.hops}
         self.Ptrue = {}
-        # ---- noise keys -> pool slices
+        # ---- noise keys -> pool slices.  Each key = a base estimate (method,
+        # pct, eps) post-processed by one cse_noise_finish job (smoothing,
+        # fix_length zero-padding, 1/max(.,eps)); base estimates are shared.
         keys = {}
         for (_, _, alg, p) in items:
             T = n_frames(L, p["hop_length"])
             keys.setdefault((p["hop_length"], noise_key(alg, p, T)), None)
         self.keys = list(keys)
-        self.pool_off, noff, tmp_need = {}, 0, 0
+        self.pool_off, noff = {}, 0
+        self.raw_off, roff = {}, 0
+        jobs = []
         for (hop, key) in self.keys:
             T = n_frames(L, hop)
+            method, pct, eps, expand, mu, inverse = key
             static = key_is_static(key)
             per_sig = B if static else T * B
             self.pool_off[(hop, key)] = (noff, 0 if static else B, per_sig)
+            base = (hop, method, pct, eps)
+            if base not in self.raw_off:
+                src_static = method in ("percentile", "simple")
+                self.raw_off[base] = (roff, 1 if src_static else T)
+                roff += S * (B if src_static else T * B)
+            r0, src_frames = self.raw_off[base]
+            jobs.append((r0, noff, src_frames, 1 if static else T, float(mu or 0.0),
+                         float(eps) if inverse else 0.0))
             noff += S * per_sig
-            method, _, _, expand, mu, inverse = key
             if method == "true_noise" and hop not in self.Ptrue:
                 if not with_clean:
                     raise ValueError("TrueNoiseEstimator requires clean_audio and noisy_audio")
                 self.Ptrue[hop] = torch.empty((S, T, B), dtype=torch.float64, device=dev)
-            if expand or mu is not None or inverse:  # chain through scratch buffers
-                tmp_need = max(tmp_need, S * T * B)
         self.pool = torch.empty(noff, dtype=torch.float32, device=dev)
-        self.scratch = torch.empty(max(tmp_need, 1), dtype=torch.float32, device=dev)
-        self.scratch2 = torch.empty(max(tmp_need, 1), dtype=torch.float32, device=dev)
+        self.raw = torch.empty(max(roff, 1), dtype=torch.float32, device=dev)
+        jt = np.zeros(len(jobs), dtype=_lib.NOISE_JOB_DTYPE)
+        for j, (so, do, sf, of, mu, ie) in enumerate(jobs):
+            jt[j] = (so, do, sf, of, mu, ie)
+        self.n_jobs = len(jobs)
+        self.jobs_d = torch.from_numpy(jt.view(np.uint8).copy()).to(dev)
+        self.med = torch.empty((S, B), dtype=torch.float64, device=dev)
         Tmax = max(n_frames(L, h) for h in self.hops)
         self.ws = torch.empty(int(eng.lib.cse_noise_workspace_bytes(S, Tmax, B)),
                               dtype=torch.uint8, device=dev)
@@ -260,49 +275,51 @@ class GridPlan:
         # frame-gain evaluations (SURVEY §8(d) unit): sum over cells of frames
         self.units = int(sum(n_frames(L, p["hop_length"]) for (_, _, _, p) in items))
 
-    def _est(self, method, P, pct, eps, out):
-        S, T, B = P.shape
-        code = {"percentile": 0, "min_tracking": 1, "true_noise": 2}[method]
-        _lib.check(self.eng.lib.cse_noise_estimate(code, _ptr(P), S, T, B, float(pct), float(eps),
-                                                   _ptr(out), _ptr(self.ws), _stream()),
-                   f"cse_noise_estimate({method})")
-
     def prepare(self, noisy, clean=None):
-        """Group-level analysis: STFTs, noise PSDs (once per signal batch)."""
+        """Group-level analysis: STFTs and every noise row (once per signal batch)."""
         eng, S, L, B = self.eng, self.S, self.L, self.B
         lib = eng.lib
+        st = _stream()
         for hop in self.hops:
             T = n_frames(L, hop)
             yv = self.Ybuf[2 * self.y_base[hop]:2 * (self.y_base[hop] + S * T * B)]
             _lib.check(lib.cse_stft(_ptr(noisy), None, S, L, self.n_fft, hop, _ptr(yv),
-                                    _ptr(self.P[hop]), _stream()), "cse_stft")
+                                    _ptr(self.P[hop]), st), "cse_stft")
             if hop in self.Ptrue:
                 _lib.check(lib.cse_stft(_ptr(noisy), _ptr(clean), S, L, self.n_fft, hop, None,
-                                        _ptr(self.Ptrue[hop]), _stream()), "cse_stft(true)")
-        for (hop, key) in self.keys:
-            method, pct, eps, expand, mu, inverse = key
-            T = n_frames(L, hop)
-            o, stride, per_sig = self.pool_off[(hop, key)]
-            dst = self.pool[o:o + S * per_sig]
-            smooth = expand or mu is not None
-            # estimate -> [smooth] -> [invert]; the last step writes the pool slice
-            est_out = dst if not (smooth or inverse) else self.scratch
-            if method == "true_noise":
-                self._est("true_noise", self.Ptrue[hop], 0.0, eps, est_out)
-            elif method == "simple":
-                self._est("percentile", self.P[hop], 25.0, eps, est_out)
-            else:
-                self._est(method, self.P[hop], pct if pct is not None else 20.0, eps, est_out)
-            cur = est_out
-            if smooth:
-                sm_out = dst if not inverse else self.scratch2
-                src_frames = 1 if method in ("percentile", "simple") else T
-                _lib.check(lib.cse_noise_smooth(_ptr(cur), S, T, B, src_frames, float(mu or 0.0),
-                                                _ptr(sm_out), _stream()), "cse_noise_smooth")
-                cur = sm_out
-            if inverse:
-                _lib.check(lib.cse_noise_invert(_ptr(cur), S * per_sig, float(eps), _ptr(dst),
-                                                _stream()), "cse_noise_invert")
+                                        _ptr(self.Ptrue[hop]), st), "cse_stft(true)")
+            bases = [b for b in self.raw_off if b[0] == hop]
+            P = self.P[hop]
+
+            def raw(b):
+                o, frames = self.raw_off[b]
+                return self.raw[o:o + S * frames * B]
+            if T >= 5 and any(m in ("percentile", "min_tracking") for (_, m, _, _) in bases):
+                _lib.check(lib.cse_noise_median(_ptr(P), S, T, B, _ptr(self.med), st),
+                           "cse_noise_median")
+            mt = [b for b in bases if b[1] == "min_tracking"]
+            for k in range(0, len(mt), 2):  # two eps per IIR + min-filter pass
+                a_, b_ = mt[k], (mt[k + 1] if k + 1 < len(mt) else None)
+                _lib.check(lib.cse_noise_min_tracking_med(
+                    _ptr(P), _ptr(self.med), S, T, B, float(a_[3]), _ptr(raw(a_)),
+                    float(b_[3]) if b_ else 0.0, _ptr(raw(b_)) if b_ else None, _ptr(self.ws),
+                    st), "cse_noise_min_tracking_med")
+            for b in bases:
+                _, method, pct, eps = b
+                if method == "percentile":
+                    _lib.check(lib.cse_noise_percentile_med(
+                        _ptr(P), _ptr(self.med), S, T, B, float(pct), float(eps), _ptr(raw(b)),
+                        _ptr(self.ws), st), "cse_noise_percentile_med")
+                elif method == "simple":
+                    _lib.check(lib.cse_noise_estimate(0, _ptr(P), S, T, B, 25.0, float(eps),
+                                                      _ptr(raw(b)), _ptr(self.ws), st),
+                               "cse_noise_estimate(simple)")
+                elif method == "true_noise":
+                    _lib.check(lib.cse_noise_estimate(2, _ptr(self.Ptrue[hop]), S, T, B, 0.0,
+                                                      float(eps), _ptr(raw(b)), None, st),
+                               "cse_noise_estimate(true)")
+        _lib.check(lib.cse_noise_finish(_ptr(self.jobs_d), self.n_jobs, S, B, _ptr(self.raw),
+                                        _ptr(self.pool), st), "cse_noise_finish")
         self.clean = clean if self.with_clean else None
 
     def enhance(self):

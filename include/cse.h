@@ -127,6 +127,47 @@ int cse_noise_smooth(const float* N, int64_t n_sig, int T, int B, int src_frames
                      float* out, cse_stream_t stream);
 
 /*
+ * Building blocks of cse_noise_estimate for the grid planner, so work shared
+ * by several estimates of one (signals, n_fft, hop) group is done once:
+ *   cse_noise_median           med[n_sig][B] = np.median(P, axis=frames)
+ *                              (noise_estimation.py:53, :93), f64;
+ *   cse_noise_percentile_med   the percentile estimate given that median (T >= 5);
+ *   cse_noise_min_tracking_med the min-tracking estimate given that median, floored
+ *                              at eps into N and (if N_b != NULL) at eps_b into N_b
+ *                              (the two eps the algorithms pass share the IIR + min
+ *                              filter, noise_estimation.py:78-94) (T >= 5).
+ * The workspace is the cse_noise_workspace_bytes() one.
+ */
+int cse_noise_median(const double* P, int64_t n_sig, int T, int B, double* med,
+                     cse_stream_t stream);
+int cse_noise_percentile_med(const double* P, const double* med, int64_t n_sig, int T, int B,
+                             double percentile, double eps, float* N, void* workspace,
+                             cse_stream_t stream);
+int cse_noise_min_tracking_med(const double* P, const double* med, int64_t n_sig, int T, int B,
+                               double eps, float* N, double eps_b, float* N_b, void* workspace,
+                               cse_stream_t stream);
+
+/*
+ * Batched post-processing of noise rows into the rows the hot kernel reads.
+ * Job j, signal s, bin b (fp64 math, f32 in/out):
+ *   x_t  = src[src_offset + (s*src_frames + t)*B + b] for t < src_frames, else 0
+ *          (src_frames = 1 for a static row that librosa fix_length zero-pads)
+ *   y_0  = x_0,  y_t = mu*y_{t-1} + (1-mu)*x_t     (mu = 0: plain copy / pad)
+ *   dst[dst_offset + (s*out_frames + t)*B + b] = inv_eps > 0 ? 1/max(y_t, inv_eps) : y_t
+ */
+typedef struct cse_noise_job {
+    int64_t src_offset;
+    int64_t dst_offset;
+    int32_t src_frames;
+    int32_t out_frames;
+    double mu;
+    double inv_eps;
+} cse_noise_job_t; /* 40 bytes */
+
+int cse_noise_finish(const cse_noise_job_t* jobs, int n_jobs, int64_t n_sig, int B,
+                     const float* src, float* dst, cse_stream_t stream);
+
+/*
  * out = 1 / max(N, eps) (fp64 math, f32 out), n elements: the noise row the
  * Wiener/MMSE/OMLSA cells of cse_enhance_cells read (their in-loop floors,
  * wiener_filter.py:122, mmse.py:71, advanced_mmse.py:207, folded in).
