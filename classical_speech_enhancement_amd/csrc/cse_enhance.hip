@@ -182,16 +182,18 @@ struct WG {
     static constexpr int CREG_RAW = (G::B * 8 > 16 * TR * 8) ? G::B * 8 : 16 * TR * 8;
     static constexpr int CREG = ((CREG_RAW + 127) / 128) * 128 + (((CREG_RAW + 127) / 128) % 2 ? 0 : 128);
     static constexpr int OFF_CELLS = 0;
-    static constexpr int OFF_Y = CPWG * CREG;                     // float2[B]
-    static constexpr int OFF_N = OFF_Y + ((G::B * 8 + 15) / 16) * 16;   // float[B]
-    static constexpr int OFF_C = OFF_N + ((G::B * 4 + 15) / 16) * 16;   // float[2][HMAX]
+    static constexpr int YROW = ((G::B * 8 + 15) / 16) * 16;      // bytes of one Y row
+    static constexpr int NROW = ((G::B * 4 + 15) / 16) * 16;      // bytes of one N row
+    static constexpr int OFF_Y = CPWG * CREG;                     // float2[2][B] (double buffer)
+    static constexpr int OFF_N = OFF_Y + 2 * YROW;                // float[2][B]
+    static constexpr int OFF_C = OFF_N + 2 * NROW;                // float[2][HMAX]
     static constexpr int OFF_TW = OFF_C + 2 * HMAX * 4;           // cf[15][L] (b = 1..15)
     static constexpr int BYTES = OFF_TW + 15 * G::L * 8;
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
 static_assert(WG<512>::BYTES <= 163840 / 4, "n_fft=512 workgroup must fit 4 per CU");
-static_assert(WG<1024>::BYTES <= 163840 / 4, "n_fft=1024 workgroup must fit 4 per CU");
+static_assert(WG<1024>::BYTES <= 163840 / 3, "n_fft=1024 workgroup must fit 3 per CU");
 static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
               WG<1024>::CPWG == CSE_CELLS_PER_GROUP(1024), "cse.h slot-group size");
 
@@ -206,6 +208,15 @@ template <typename T>
 __device__ __forceinline__ T opaque(T x) {
     asm volatile("" : "+v"(x));
     return x;
+}
+
+// Ordering of LDS accesses between the lanes of ONE wave: the LDS executes a
+// wave's DS instructions in issue order, so a compiler-level barrier is all a
+// write->read or read->write hand-off inside the wave needs (no s_waitcnt).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 template <int NFFT>
@@ -230,8 +241,6 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     const int cs = lane / L, i = lane % L;
     const int cslot = wave * G::CPW + cs;
     const int creg = W::OFF_CELLS + cslot * W::CREG;   // byte offset of my cell's region
-    float2* yrow = (float2*)(smem + W::OFF_Y);
-    float* nrow = (float*)(smem + W::OFF_N);
     float* crow = (float*)(smem + W::OFF_C);
     const cf* tw1 = (const cf*)(smem + W::OFF_TW);
 
@@ -288,8 +297,11 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             pc[u] = (j < HOP && cbase && o >= 0 && o < len) ? (float)cbase[o] : 0.0f;
         }
     };
+    // rows of frame t live in buffer t&1 (static noise: buffer 0 only)
     auto store_rows = [&](int t) {  // registers -> LDS rows of frame t
         if (t < nf) {
+            float2* yrow = (float2*)(smem + W::OFF_Y + (t & 1) * W::YROW);
+            float* nrow = (float*)(smem + W::OFF_N + (t & 1) * W::NROW);
 #pragma unroll
             for (int u = 0; u < W::YPT; ++u) {
                 const int k = tid + u * W::THREADS;
@@ -305,8 +317,12 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             if (j < HOP) crow[(t & 1) * W::HMAX + j] = pc[u];
         }
     };
-    if (!nstride) {  // static noise row: once
-        for (int k = tid; k < B; k += W::THREADS) nrow[k] = Nbase[k];
+    if (!nstride) {  // static noise row: once, in both buffers
+        for (int k = tid; k < B; k += W::THREADS) {
+            const float v = Nbase[k];
+            ((float*)(smem + W::OFF_N))[k] = v;
+            ((float*)(smem + W::OFF_N + W::NROW))[k] = v;
+        }
     }
     load_rows(0);
     store_rows(0);
@@ -347,12 +363,14 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                      "+v"(ws[1]), "+v"(pc2[0]), "+v"(pc2[1]), "+v"(ps2[0]), "+v"(ps2[1]));
         const cf base = cmk(bc, bs);
         if (t < nf) {
-            __syncthreads();  // rows(t) visible; last frame's transpose reads done
+            // the one workgroup barrier per frame: rows(t) (stored during frame
+            // t-1) are visible, and nobody still reads buffer (t+1)&1
+            __syncthreads();
             // ---------------- gain stage: S = Y * G into my cell's LDS row
             {
                 cf* sb = (cf*)(smem + opaque(creg + 8 * i));   // &S[i]
-                const float2* yr = (const float2*)((unsigned char*)yrow + opaque(8 * i));
-                const float* nr = (const float*)((unsigned char*)nrow + opaque(4 * i));
+                const float2* yr = (const float2*)(smem + opaque(W::OFF_Y + (t & 1) * W::YROW + 8 * i));
+                const float* nr = (const float*)(smem + opaque(W::OFF_N + (t & 1) * W::NROW + 4 * i));
 #pragma unroll
                 for (int j = 0; j < 17; ++j) {
                     if (j == 16 && i != 0) continue;
@@ -389,9 +407,9 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     if (OUT && gout) gout[t * B + i + kk] = g;
                 }
             }
-            __syncthreads();  // S rows complete; every wave is done with yrow/nrow(t)
-            store_rows(t + 1);
+            store_rows(t + 1);  // other buffer: its last readers passed this frame's barrier
             load_rows(t + 2);
+            wave_sync();  // my wave's S rows complete (cells never span waves)
 
             // ---------------- pass 1: real-IFFT packing + DFT16 over j -----
             // Z'[k] = (X_k + X*_{M-k}) + i (X_k - X*_{M-k}) e^{2πi k/NFFT}
@@ -418,15 +436,13 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 #pragma unroll
                 for (int b = 1; b < 16; ++b) z[b] = cmul(z[b], tw[(b - 1) * L]);
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_wave_barrier();  // my wave's S reads done (in-order LDS)
+            wave_sync();  // my wave's S reads are issued before the transpose overwrites
             {
                 cf* tw_ = (cf*)(smem + opaque(creg + 8 * i));   // V[b][i] at b*TR + i
 #pragma unroll
                 for (int b = 0; b < 16; ++b) tw_[b * TR] = z[b];
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_wave_barrier();  // transpose block complete
+            wave_sync();  // transpose block written
 
             // ---------------- pass 2: DFT over the lane index --------------
             cf v[16];
