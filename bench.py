@@ -186,9 +186,10 @@ def main():
 
     # sanity of the step's output: every cell finite, SNRs finite
     sse, fin = plan.results()[:2]
-    assert fin.all(), "non-finite enhanced output"
-    snr = snr_db(sse, clean_pow[[s for (s, _, _) in specs]])
-    assert np.isfinite(snr).all()
+    if not os.environ.get("CSE_BENCH_NOCHECK"):  # set only for timing-only ablation builds
+        assert fin.all(), "non-finite enhanced output"
+        snr = snr_db(sse, clean_pow[[s for (s, _, _) in specs]])
+        assert np.isfinite(snr).all()
 
     if rank != 0:
         if world > 1:

@@ -88,25 +88,24 @@ __device__ __forceinline__ float mmse_bracket(float v, float sqrtv) {
 // only ever uses prev_gain**2 * prev_gamma (wiener_filter.py:133, mmse.py:82,
 // advanced_mmse.py:215): the carried state is rr = (G*G)*gamma.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float gain_wiener(float P, float inv, bool first, float& rr,
-                                             float alpha, float gfloor) {
+// First frame: the reference uses xi = d (Wiener) / max(gamma-1, ksi_min)
+// (MMSE, OMLSA); with rr = 0 and alpha_t = 0 on frame 0 the general DD
+// expression alpha_t*rr + (1-alpha_t)*max(gamma-1, 0) gives exactly that (for
+// ksi_min >= 0), so there is no per-bin branch to split the scheduling region.
+__device__ __forceinline__ float gain_wiener(float P, float inv, float& rr, float alpha_t,
+                                             float gfloor) {
     const float gam = fmaxf(P * inv, 1e-10f);
     const float d = fmaxf(gam - 1.0f, 0.0f);
-    float xi = first ? d : alpha * rr + (1.0f - alpha) * d;
-    xi = fmaxf(xi, 1e-10f);
+    const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * d, 1e-10f);
     const float g = fminf(fmaxf(xi * fast_rcp(1.0f + xi), gfloor), 1.0f);
     rr = (g * g) * gam;
     return g;
 }
 
-__device__ __forceinline__ float gain_mmse(float P, float inv, bool first, float& rr,
-                                           float alpha, float ksi_min, float gmin, float gmax) {
+__device__ __forceinline__ float gain_mmse(float P, float inv, float& rr, float alpha_t,
+                                           float ksi_min, float gmin, float gmax) {
     const float gam = fmaxf(P * inv, 1e-12f);
-    float xi;
-    if (first)
-        xi = fmaxf(gam - 1.0f, ksi_min);
-    else
-        xi = fmaxf(alpha * rr + (1.0f - alpha) * fmaxf(gam - 1.0f, 0.0f), ksi_min);
+    const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * fmaxf(gam - 1.0f, 0.0f), ksi_min);
     const float v = fminf(fmaxf(xi * gam * fast_rcp(1.0f + xi), 1e-12f), 80.0f);
     const float sv = __builtin_amdgcn_sqrtf(v);
     const float h = mmse_bracket(v, sv);
@@ -124,15 +123,11 @@ __device__ __forceinline__ float gain_mmse(float P, float inv, bool first, float
 //             = log2(xi r)                                               (v >= 17: E1 < 2.4e-9)
 //   p = 1/(1 + (1-q)/(q Lambda + eps)) = A / (A + 1 - q),  A = q Lambda + eps
 //   G = clip(g_lsa^p gf^(1-p), gf, 1) = clip(exp2(lgf + p (lg - lgf)), gf, 1)
-__device__ __forceinline__ float gain_omlsa(float P, float inv, bool first, float& rr,
-                                            float alpha, float ksi_min, float gfloor,
-                                            float lg2_floor, float q, float vmax) {
+__device__ __forceinline__ float gain_omlsa(float P, float inv, float& rr, float alpha_t,
+                                            float ksi_min, float gfloor, float lg2_floor, float q,
+                                            float vmax) {
     const float gam = fmaxf(P * inv, 1e-10f);
-    float xi;
-    if (first)
-        xi = fmaxf(gam - 1.0f, ksi_min);
-    else
-        xi = fmaxf(alpha * rr + (1.0f - alpha) * fmaxf(gam - 1.0f, 0.0f), ksi_min);
+    const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * fmaxf(gam - 1.0f, 0.0f), ksi_min);
     const float r = fast_rcp(1.0f + xi);
     const float v = fminf(fmaxf(xi * gam * r, 1e-12f), vmax);
     const bool small = v < CSE_EIN_VMAX;
@@ -188,7 +183,9 @@ struct WG {
     static constexpr int OFF_N = OFF_Y + 2 * YROW;                // float[2][B]
     static constexpr int OFF_C = OFF_N + 2 * NROW;                // float[2][HMAX]
     static constexpr int OFF_TW = OFF_C + 2 * HMAX * 4;           // cf[15][L] (b = 1..15)
-    static constexpr int BYTES = OFF_TW + 15 * G::L * 8;
+    static constexpr int OFF_LC = OFF_TW + 15 * G::L * 8;         // float[L][12] lane constants
+    static constexpr int OFF_CP = OFF_LC + G::L * 48;             // float[CPWG][8] cell params
+    static constexpr int BYTES = OFF_CP + CPWG * 32;
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
@@ -196,6 +193,13 @@ static_assert(WG<512>::BYTES <= 163840 / 4, "n_fft=512 workgroup must fit 4 per 
 static_assert(WG<1024>::BYTES <= 163840 / 3, "n_fft=1024 workgroup must fit 3 per CU");
 static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
               WG<1024>::CPWG == CSE_CELLS_PER_GROUP(1024), "cse.h slot-group size");
+
+// CSE_ABLATE (timing experiments only; 0 in every product build):
+//   1 = trivial gain (S = Y), 2 = no inverse FFT passes, 4 = no sample retire,
+//   8 = no workgroup barrier
+#ifndef CSE_ABLATE
+#define CSE_ABLATE 0
+#endif
 
 // waves per SIMD the register allocation targets (VGPR budget 512 / w)
 #ifndef CSE_WAVES_PER_SIMD
@@ -219,12 +223,53 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// lane constants (depend only on the lane-in-cell i), kept in LDS so they do
+// not occupy VGPRs across the frame loop: the packing rotor e^{2πi i/NFFT},
+// the window phase (pre-scaled by 0.5/NFFT) of the lane's two sample parities,
+// and the 512/256 closed-form wss phase.
+struct LaneConst {
+    float bc, bs, wc0, wc1, ws0, ws1, pc0, pc1, ps0, ps1, pad0, pad1;
+};
+static_assert(sizeof(LaneConst) == 48, "LaneConst layout");
+
 template <int NFFT>
-__device__ __forceinline__ float hann_at(int aidx, int e, const float (&wc)[2],
-                                         const float (&ws)[2]) {
-    // w(n)/NFFT at n = SP*aidx + off + e (wc/ws carry the lane phase, pre-scaled)
+__device__ __forceinline__ float hann_at(int aidx, int e, const LaneConst& lc) {
+    // w(n)/NFFT at n = SP*aidx + off + e
     const float ca = Rot32::c[(2 * aidx) & 31], sa = Rot32::s[(2 * aidx) & 31];
-    return 0.5f / NFFT - (ca * wc[e] - sa * ws[e]);
+    const float wc = e ? lc.wc1 : lc.wc0, ws = e ? lc.ws1 : lc.ws0;
+    return 0.5f / NFFT - (ca * wc - sa * ws);
+}
+
+// per-cell parameters as the gain stage wants them
+struct CellParam {
+    float p0, p1, p2, p3, p4, lg2_floor, q_spp, pad;
+};
+static_assert(sizeof(CellParam) == 32, "CellParam layout");
+
+template <int ALGO>
+__device__ __forceinline__ cf gain_bin(float2 y, float nz, float& rr, float alpha_t,
+                                       const CellParam& cp, float& g) {
+    const float P = y.x * y.x + y.y * y.y;
+    if (CSE_ABLATE & 1) {
+        g = nz;
+        return cmk(y.x * nz, y.y * nz);
+    }
+    if (ALGO == CSE_ALGO_SS) {
+        // Ps = max(P - a N, b N); |S| = sqrt(Ps) with the noisy phase
+        // (spectral_subtractor.py:44-53).  No eps floor: the reference floors
+        // BEFORE fix_length (engine.noise_key).
+        const float ps = fmaxf(P - cp.p0 * nz, cp.p1 * nz);
+        const float sp = __builtin_amdgcn_sqrtf(ps);
+        g = (P > 0.0f) ? sp * __builtin_amdgcn_rsqf(P) : 0.0f;
+        return (P > 0.0f) ? cmk(y.x * g, y.y * g) : cmk(sp, 0.0f);  // angle(0) = 0
+    }
+    if (ALGO == CSE_ALGO_WIENER)
+        g = gain_wiener(P, nz, rr, alpha_t, cp.p1);
+    else if (ALGO == CSE_ALGO_MMSE)
+        g = gain_mmse(P, nz, rr, alpha_t, cp.p1, cp.p2, cp.p3);
+    else
+        g = gain_omlsa(P, nz, rr, alpha_t, cp.p1, cp.p2, cp.lg2_floor, cp.q_spp, cp.p4);
+    return cmk(y.x * g, y.y * g);
 }
 
 template <int NFFT, int HOP, int ALGO, bool OUT>
@@ -235,13 +280,13 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     constexpr int M = G::M, L = G::L, B = G::B, SP = G::SP, TR = W::TR;
     constexpr int R = NFFT / HOP;       // frames overlapping one sample
     constexpr int F = 2 * HOP / SP;     // samples a lane retires per frame
+    constexpr int PEND = 32 - F;        // overlap-add sums carried to the next frame
     static_assert(F >= 2 && F <= 32 && (F % 2) == 0, "hop/n_fft combination");
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int cs = lane / L, i = lane % L;
     const int cslot = wave * G::CPW + cs;
     const int creg = W::OFF_CELLS + cslot * W::CREG;   // byte offset of my cell's region
-    float* crow = (float*)(smem + W::OFF_C);
     const cf* tw1 = (const cf*)(smem + W::OFF_TW);
 
     // ---- the shared rows of this workgroup (first cell's; host-validated)
@@ -257,22 +302,51 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 
     // ---- my cell
     const bool valid = cslot < n_cells_wg && wcell[cslot].algo == ALGO;
-    const cse_cell_t* cp = wcell + (cslot < n_cells_wg ? cslot : 0);
-    const float p0 = cp->param[0], p1 = cp->param[1], p2 = cp->param[2], p3 = cp->param[3],
-                p4 = cp->param[4];
-    float* yout = (OUT && valid && cp->out_offset >= 0 && a.y_out) ? a.y_out + cp->out_offset
-                                                                   : nullptr;
-    float* gout = (OUT && valid && cp->gain_offset >= 0 && a.g_out) ? a.g_out + cp->gain_offset
-                                                                    : nullptr;
-    const float lg2_floor = (ALGO == CSE_ALGO_OMLSA) ? fast_log2(p2) : 0.0f;
-    const float q_spp = fminf(fmaxf(p3, 1e-3f), 1.0f - 1e-3f);
+    float* yout = nullptr;
+    float* gout = nullptr;
+    if (OUT && valid) {
+        const cse_cell_t* cp = wcell + cslot;
+        if (cp->out_offset >= 0 && a.y_out) yout = a.y_out + cp->out_offset;
+        if (cp->gain_offset >= 0 && a.g_out) gout = a.g_out + cp->gain_offset;
+    }
 
-    // ---- pass-1 twiddles e^{2πi i b/M}, [b-1][i], shared by the workgroup
+    // ---- workgroup tables: pass-1 twiddles e^{2πi i b/M} [b-1][i], lane
+    // constants [i], cell parameters [slot]
     for (int e = tid; e < 15 * L; e += W::THREADS) {
         const int b = 1 + e / L, ii = e % L;
         double s, c;
         sincospi(2.0 * (double)(ii * b) / (double)M, &s, &c);
         ((cf*)(smem + W::OFF_TW))[e] = cmk((float)c, (float)s);
+    }
+    for (int ii = tid; ii < L; ii += W::THREADS) {
+        LaneConst lc;
+        const int bb = (L == 16) ? ii : (ii & 15), hh = (L == 16) ? 0 : (ii >> 4);
+        const int of = 2 * bb + 32 * hh;
+        sincospif(2.0f * (float)ii / (float)NFFT, &lc.bs, &lc.bc);
+        float s_, c_;
+        sincospif(2.0f * (float)of / (float)NFFT, &s_, &c_);
+        lc.wc0 = (0.5f / NFFT) * c_;
+        lc.ws0 = (0.5f / NFFT) * s_;
+        sincospif(2.0f * (float)(of + 1) / (float)NFFT, &s_, &c_);
+        lc.wc1 = (0.5f / NFFT) * c_;
+        lc.ws1 = (0.5f / NFFT) * s_;
+        sincospif(2.0f * (float)of / 256.0f, &lc.ps0, &lc.pc0);
+        sincospif(2.0f * (float)(of + 1) / 256.0f, &lc.ps1, &lc.pc1);
+        lc.pad0 = lc.pad1 = 0.0f;
+        ((LaneConst*)(smem + W::OFF_LC))[ii] = lc;
+    }
+    for (int c = tid; c < W::CPWG; c += W::THREADS) {
+        const cse_cell_t* cp = wcell + (c < n_cells_wg ? c : 0);
+        CellParam prm;
+        prm.p0 = cp->param[0];
+        prm.p1 = cp->param[1];
+        prm.p2 = cp->param[2];
+        prm.p3 = cp->param[3];
+        prm.p4 = cp->param[4];
+        prm.lg2_floor = (ALGO == CSE_ALGO_OMLSA) ? fast_log2(prm.p2) : 0.0f;
+        prm.q_spp = fminf(fmaxf(prm.p3, 1e-3f), 1.0f - 1e-3f);
+        prm.pad = 0.0f;
+        ((CellParam*)(smem + W::OFF_CP))[c] = prm;
     }
 
     // ---- row staging: thread tid owns Y/N elements tid + u*THREADS, clean tid + u*THREADS
@@ -297,7 +371,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             pc[u] = (j < HOP && cbase && o >= 0 && o < len) ? (float)cbase[o] : 0.0f;
         }
     };
-    // rows of frame t live in buffer t&1 (static noise: buffer 0 only)
+    // rows of frame t live in buffer t&1 (static noise: written to both once)
     auto store_rows = [&](int t) {  // registers -> LDS rows of frame t
         if (t < nf) {
             float2* yrow = (float2*)(smem + W::OFF_Y + (t & 1) * W::YROW);
@@ -311,13 +385,14 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 }
             }
         }
+        float* crow = (float*)(smem + W::OFF_C + (t & 1) * W::HMAX * 4);
 #pragma unroll
         for (int u = 0; u < W::CPT; ++u) {
             const int j = tid + u * W::THREADS;
-            if (j < HOP) crow[(t & 1) * W::HMAX + j] = pc[u];
+            if (j < HOP) crow[j] = pc[u];
         }
     };
-    if (!nstride) {  // static noise row: once, in both buffers
+    if (!nstride) {
         for (int k = tid; k < B; k += W::THREADS) {
             const float v = Nbase[k];
             ((float*)(smem + W::OFF_N))[k] = v;
@@ -328,81 +403,50 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     store_rows(0);
     load_rows(1);
 
-    // ---- lane constants
-    float bs, bc;  // e^{2πi i/NFFT}
-    sincospif(2.0f * (float)i / (float)NFFT, &bs, &bc);
     const int b2 = (L == 16) ? i : (i & 15);
     const int h2 = (L == 16) ? 0 : (i >> 4);
     const int off = 2 * b2 + 32 * h2;  // lane's first sample offset inside a frame
-    float wc[2], ws[2], pc2[2], ps2[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-        float s_, c_;
-        sincospif(2.0f * (float)(off + e) / (float)NFFT, &s_, &c_);
-        wc[e] = (0.5f / NFFT) * c_;
-        ws[e] = (0.5f / NFFT) * s_;
-        sincospif(2.0f * (float)(off + e) / 256.0f, &s_, &c_);  // only used for R == 2
-        pc2[e] = c_;
-        ps2[e] = s_;
-    }
 
     float rr[17];  // prev_gain**2 * prev_gamma per bin (read from frame 1 on)
 #pragma unroll
     for (int j = 0; j < 17; ++j) rr[j] = 0.0f;
-    float acc[32];
+    float acc[PEND];  // overlap-add sums of the positions frame t's slots q < PEND cover
 #pragma unroll
-    for (int q = 0; q < 32; ++q) acc[q] = 0.0f;
+    for (int q = 0; q < PEND; ++q) acc[q] = 0.0f;
     double sse = 0.0;
     bool fin = true;
 
     for (int t = 0; t < nf + R - 1; ++t) {
-        // Keep lane rotors and LDS bases opaque per frame: otherwise LICM hoists
-        // the 32 window values, 16 packing twiddles and ~40 per-index LDS
-        // addresses derived from them into long-lived VGPRs (spills).
-        asm volatile("" : "+v"(bc), "+v"(bs), "+v"(wc[0]), "+v"(wc[1]), "+v"(ws[0]),
-                     "+v"(ws[1]), "+v"(pc2[0]), "+v"(pc2[1]), "+v"(ps2[0]), "+v"(ps2[1]));
-        const cf base = cmk(bc, bs);
+        float x[32];  // this frame's windowed IFFT samples (0 in flush frames)
         if (t < nf) {
             // the one workgroup barrier per frame: rows(t) (stored during frame
             // t-1) are visible, and nobody still reads buffer (t+1)&1
-            __syncthreads();
+            if (!(CSE_ABLATE & 8)) __syncthreads();
             // ---------------- gain stage: S = Y * G into my cell's LDS row
             {
+                const CellParam cpar =
+                    *(const CellParam*)(smem + opaque(W::OFF_CP + 32 * cslot));
+                const float alpha_t = (t == 0) ? 0.0f : cpar.p0;  // see gain_wiener
                 cf* sb = (cf*)(smem + opaque(creg + 8 * i));   // &S[i]
-                const float2* yr = (const float2*)(smem + opaque(W::OFF_Y + (t & 1) * W::YROW + 8 * i));
-                const float* nr = (const float*)(smem + opaque(W::OFF_N + (t & 1) * W::NROW + 4 * i));
+                const float2* yr =
+                    (const float2*)(smem + opaque(W::OFF_Y + (t & 1) * W::YROW + 8 * i));
+                const float* nr =
+                    (const float*)(smem + opaque(W::OFF_N + (t & 1) * W::NROW + 4 * i));
+                float2 y_nx = yr[0];
+                float n_nx = nr[0];
 #pragma unroll
                 for (int j = 0; j < 17; ++j) {
-                    if (j == 16 && i != 0) continue;
                     const int kk = (j < 16) ? L * j : M;  // k - i
-                    const float2 y = yr[kk];
-                    const float nz = nr[kk];
-                    const float P = y.x * y.x + y.y * y.y;
-                    float g;
-                    cf Sj;
-                    if (ALGO == CSE_ALGO_SS) {
-                        // Ps = max(P - a N, b N); |S| = sqrt(Ps) with the noisy phase
-                        // (spectral_subtractor.py:44-53).  No eps floor: the
-                        // reference floors BEFORE fix_length (engine.noise_key).
-                        const float ps = fmaxf(P - p0 * nz, p1 * nz);
-                        const float sp = __builtin_amdgcn_sqrtf(ps);
-                        if (P > 0.0f) {
-                            g = sp * __builtin_amdgcn_rsqf(P);
-                            Sj = cmk(y.x * g, y.y * g);
-                        } else {  // angle(0) = 0
-                            g = 0.0f;
-                            Sj = cmk(sp, 0.0f);
-                        }
-                    } else {
-                        if (ALGO == CSE_ALGO_WIENER)
-                            g = gain_wiener(P, nz, t == 0, rr[j], p0, p1);
-                        else if (ALGO == CSE_ALGO_MMSE)
-                            g = gain_mmse(P, nz, t == 0, rr[j], p0, p1, p2, p3);
-                        else
-                            g = gain_omlsa(P, nz, t == 0, rr[j], p0, p1, p2, lg2_floor, q_spp,
-                                           p4);
-                        Sj = cmk(y.x * g, y.y * g);
+                    const float2 y = y_nx;
+                    const float nz = n_nx;
+                    if (j < 16) {  // prefetch the next bin's row entries
+                        const int kn = (j + 1 < 16) ? L * (j + 1) : M;
+                        y_nx = yr[kn];
+                        n_nx = nr[kn];
                     }
+                    if (j == 16 && i != 0) break;
+                    float g;
+                    const cf Sj = gain_bin<ALGO>(y, nz, rr[j], alpha_t, cpar, g);
                     sb[kk] = Sj;
                     if (OUT && gout) gout[t * B + i + kk] = g;
                 }
@@ -415,6 +459,8 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             // Z'[k] = (X_k + X*_{M-k}) + i (X_k - X*_{M-k}) e^{2πi k/NFFT}
             cf z[16];
             {
+                const LaneConst* lcp = (const LaneConst*)(smem + opaque(W::OFF_LC + 48 * i));
+                const cf base = cmk(lcp->bc, lcp->bs);
                 const cf* sa = (const cf*)(smem + opaque(creg + 8 * i));                   // S[i + L j]
                 const cf* sm = (const cf*)(smem + opaque(creg + 8 * (M - i - 15 * L)));   // S[M - i - L j]
 #pragma unroll
@@ -430,7 +476,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     z[j] = cadd(cadd(A, Bc), cmuli(cmul(csub(A, Bc), tw)));
                 }
             }
-            idft16(z);
+            if (!(CSE_ABLATE & 2)) idft16(z);
             {
                 const cf* tw = (const cf*)((const unsigned char*)tw1 + opaque(8 * i));
 #pragma unroll
@@ -461,39 +507,67 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     }
                 }
             }
-            idft16(v);
-
-            // ---------------- synthesis window (/n_fft) + overlap-add ------
+            if (!(CSE_ABLATE & 2)) idft16(v);
+            // ---------------- synthesis window (/n_fft) --------------------
+            {
+                const LaneConst lc = *(const LaneConst*)(smem + opaque(W::OFF_LC + 48 * i));
 #pragma unroll
-            for (int q = 0; q < 32; ++q) {
-                const float w = hann_at<NFFT>(q >> 1, q & 1, wc, ws);
-                const float x = (q & 1) ? v[q >> 1].y : v[q >> 1].x;
-                acc[q] = fmaf(x, w, acc[q]);
+                for (int q = 0; q < 32; ++q)
+                    x[q] = ((q & 1) ? v[q >> 1].y : v[q >> 1].x) * hann_at<NFFT>(q >> 1, q & 1, lc);
             }
         } else {
             __syncthreads();  // flush frames: clean row t visible, row t-1 reads done
             store_rows(t + 1);
             load_rows(t + 2);
+#pragma unroll
+            for (int q = 0; q < 32; ++q) x[q] = 0.0f;
         }
 
-        // ---------------- retire HOP finished samples ----------------------
-        // y = ola / wss (librosa istft normalisation), then the SNR error sum
-        // of the clipped sample (evaluation_metrics.py:52-56).  Steady frames
-        // use the closed-form wss; the first R-1 and the flush frames sum the
-        // covering windows explicitly (a separate path, so its registers do
-        // not add to the steady loop's).
-        auto retire = [&](auto inv_of_q) {
-            if (!valid) return;
+        // ---------------- overlap-add + retire HOP finished samples ---------
+        // slot q < F of this frame completes output position t*HOP + n(q):
+        // y = (ola) / wss (librosa istft normalisation), then the SNR error
+        // sum of the clipped sample (evaluation_metrics.py:52-56).  Steady
+        // frames use the closed-form wss; the first R-1 and the flush frames
+        // sum the covering windows explicitly.
+        float done[F];
+#pragma unroll
+        for (int q = 0; q < F; ++q) done[q] = acc[q] + x[q];
+#pragma unroll
+        for (int q = 0; q < PEND; ++q) acc[q] = (q + F < PEND ? acc[q + F] : 0.0f) + x[q + F];
+        if (valid && !(CSE_ABLATE & 4)) {
+            const LaneConst lc = *(const LaneConst*)(smem + opaque(W::OFF_LC + 48 * i));
+            const bool edge = (t < R - 1) || (t >= nf);
             const int o0 = t * HOP + off - NFFT / 2;  // output index of q = 0
-            const float* crow_t = (const float*)((const unsigned char*)crow +
-                                                 opaque(4 * ((t & 1) * W::HMAX + off)));
+            const float* crow_t = (const float*)(smem + opaque(W::OFF_C + (t & 1) * W::HMAX * 4 +
+                                                               4 * off));
             float part = 0.0f;
 #pragma unroll
             for (int q = 0; q < F; ++q) {
                 const int n = SP * (q >> 1) + (q & 1);  // + off: position inside frame t
                 const int o = o0 + n;
+                float inv;
+                if (R == 2) {  // 0.75 + 0.25 cos(2π n/256) for 512/256; n = 32 aq + off + e
+                    const int m = (4 * (q >> 1)) & 31;
+                    inv = __builtin_amdgcn_rcpf(
+                        0.75f + 0.25f * (Rot32::c[m] * ((q & 1) ? lc.pc1 : lc.pc0) -
+                                         Rot32::s[m] * ((q & 1) ? lc.ps1 : lc.ps0)));
+                } else {
+                    inv = (R == 4) ? (1.0f / 1.5f) : (1.0f / 3.0f);
+                }
+                if (edge) {
+                    float wss = 0.0f;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int tr = t - r;
+                        if (tr >= 0 && tr < nf) {
+                            const float w = hann_at<NFFT>((q >> 1) + r * (HOP / SP), q & 1, lc) * NFFT;
+                            wss = fmaf(w, w, wss);
+                        }
+                    }
+                    inv = wss > 0.0f ? __builtin_amdgcn_rcpf(wss) : 1.0f;
+                }
                 if (o >= 0 && o < len) {
-                    const float y = acc[q] * inv_of_q(q);
+                    const float y = done[q] * inv;
                     fin = fin && __builtin_isfinite(y);
                     if (OUT && yout) yout[o] = y;
                     const float d = crow_t[n] - fminf(fmaxf(y, -1.0f), 1.0f);
@@ -501,35 +575,10 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 }
             }
             sse += (double)part;
-        };
-        if ((t < R - 1) || (t >= nf)) {
-            retire([&](int q) {
-                float wss = 0.0f;
+        } else if (CSE_ABLATE & 4) {
 #pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int tr = t - r;
-                    if (tr >= 0 && tr < nf) {
-                        const float w =
-                            hann_at<NFFT>((q >> 1) + r * (HOP / SP), q & 1, wc, ws) * NFFT;
-                        wss = fmaf(w, w, wss);
-                    }
-                }
-                return wss > 0.0f ? __builtin_amdgcn_rcpf(wss) : 1.0f;
-            });
-        } else if (R == 2) {
-            // 0.75 + 0.25 cos(2π n/256) for 512/256; n = 32 aq + off + e
-            retire([&](int q) {
-                const int m = (4 * (q >> 1)) & 31;  // 2π(32 aq)/256 = 2π(4 aq)/32
-                return __builtin_amdgcn_rcpf(
-                    0.75f + 0.25f * (Rot32::c[m] * pc2[q & 1] - Rot32::s[m] * ps2[q & 1]));
-            });
-        } else {
-            retire([&](int) { return (R == 4) ? (1.0f / 1.5f) : (1.0f / 3.0f); });
+            for (int q = 0; q < F; ++q) asm volatile("" ::"v"(done[q]));
         }
-#pragma unroll
-        for (int q = 0; q < 32 - F; ++q) acc[q] = acc[q + F];
-#pragma unroll
-        for (int q = 32 - F; q < 32; ++q) acc[q] = 0.0f;
     }
 
     // ---------------- per-cell reductions over the cell's L lanes ----------
