@@ -1,0 +1,235 @@
+"""Grid-search driver: the data-parallel rewrite of the reference's sweep.
+
+The reference walks pairs -> algorithms -> parameter combinations one cell at
+a time (speech_enhancement_comparison.py:149-226 inside optimize_parameters,
+called per algorithm from run_algorithm_on_pair :275-292 and main :395-430).
+Here the whole (pair x algorithm x grid cell) set is one job:
+
+  job_specs      the reference's enumeration order; a cell's index in this
+                 list is its cell_id (grid order inside each (pair, algorithm))
+  work_items     cells grouped by what they share on the device:
+                 (pair, n_fft, hop, algorithm) -> one STFT, one set of noise
+                 rows; cost = cells x frames x bins x algorithm weight
+  assign_lpt     greedy longest-processing-time assignment of items to ranks
+                 (SURVEY §8(e)); an item larger than total/(2*world) is split
+                 in cell chunks first (splitting only repeats one STFT)
+  run_grid       each rank computes its cells (Engine on its GPU), then ONE
+                 all_gather of fixed-size records {cell_id, sse, snr, finite}
+                 (RCCL over xGMI for backend "nccl", gloo in CPU tests)
+  select_best    rank 0's sequential best-so-far scan in grid order
+                 (speech_enhancement_comparison.py:183-216) — NOT an argmax:
+                 a later cell replaces the incumbent only if it beats it by
+                 more than tol, so ties within tol keep the earlier cell
+
+Scores: the reference scores cells by STOI, PESQ and their balance
+(evaluation_metrics.py:30-36, 104-115); pystoi/pesq are not available in this
+image, so the device path scores by SNR of the clipped output
+(evaluation_metrics.py:39-58), the metric the reference reports next to them.
+The SNR here is taken at lag 0 (the synthetic pairs are aligned); the
+cross-correlation alignment of finalize_enhanced (:38-69) is the next §8(f)
+row and is applied on the host in the oracle only.
+"""
+
+import math
+from collections import OrderedDict
+
+import numpy as np
+
+from .parameter_ranges import ALGORITHM_GRIDS, grid_cells
+
+# per-bin cost weights (measured kernel time per frame, OMLSA ~ 3x SS)
+ALGO_WEIGHT = {"spectralSubtractor": 1.0, "wiener": 1.1, "mmse": 2.0, "omlsa": 3.0}
+# tolerance of the best-so-far update per objective (speech_enhancement_comparison.py:183,194,205)
+TOLERANCE = {"stoi": 1e-6, "pesq": 1e-3, "balance": 1e-5, "snr": 1e-5}
+
+RECORD_FIELDS = ("cell_id", "sse", "snr", "finite")  # one float64 row per cell
+
+
+def job_specs(n_pairs, algorithms=None, grids=None, n_fft=None):
+    """(pair, algorithm, params) for every pair x algorithm x grid cell, in the
+    reference's order (pairs outermost, registry order of algorithms, grid
+    order with the last key fastest)."""
+    grids = grids or ALGORITHM_GRIDS
+    algorithms = list(algorithms or grids)
+    out = []
+    for pair in range(n_pairs):
+        for alg in algorithms:
+            for p in grid_cells(grids[alg]):
+                if n_fft is None or p["n_fft"] == n_fft:
+                    out.append((pair, alg, p))
+    return out
+
+
+def frames(length, hop):
+    return 1 + int(length) // int(hop)
+
+
+def work_items(specs, lengths):
+    """Group cell ids by (pair, n_fft, hop, algorithm).  Returns a list of
+    (cost, [cell ids]) in first-appearance order."""
+    groups = OrderedDict()
+    for cid, (pair, alg, p) in enumerate(specs):
+        key = (pair, int(p["n_fft"]), int(p["hop_length"]), alg)
+        groups.setdefault(key, []).append(cid)
+    items = []
+    for (pair, n_fft, hop, alg), ids in groups.items():
+        per_cell = frames(lengths[pair], hop) * (n_fft // 2 + 1) * ALGO_WEIGHT.get(alg, 1.0)
+        items.append((per_cell * len(ids), ids))
+    return items
+
+
+def assign_lpt(specs, lengths, world):
+    """Rank of every cell: items (split when > total/(2*world)) handed out
+    largest-first to the least-loaded rank (ties -> lowest rank)."""
+    items = work_items(specs, lengths)
+    total = sum(c for c, _ in items)
+    cap = total / (2.0 * world) if world > 1 else math.inf
+    pieces = []
+    for cost, ids in items:
+        n = max(1, int(math.ceil(cost / cap))) if cap < math.inf else 1
+        n = min(n, len(ids))
+        per = int(math.ceil(len(ids) / n))
+        unit = cost / len(ids)
+        for s in range(0, len(ids), per):
+            chunk = ids[s:s + per]
+            pieces.append((unit * len(chunk), chunk[0], chunk))
+    pieces.sort(key=lambda x: (-x[0], x[1]))
+    load = [0.0] * world
+    rank_of = np.empty(len(specs), dtype=np.int64)
+    for cost, _, chunk in pieces:
+        r = min(range(world), key=lambda k: (load[k], k))
+        load[r] += cost
+        rank_of[chunk] = r
+    return rank_of, load
+
+
+def engine_compute(clean, noisy, specs, ids, engine=None):
+    """Device compute of the cells ``ids``: per-cell (sse, snr, finite).
+
+    clean/noisy: lists of 1-D float arrays (host) indexed by pair.  Pairs are
+    batched by length (the engine's signal batches are rectangular)."""
+    import torch
+    from .engine import Engine, snr_db
+    eng = engine or Engine()
+    out = np.zeros((len(ids), 3))
+    by_len = OrderedDict()
+    for j, cid in enumerate(ids):
+        pair = specs[cid][0]
+        by_len.setdefault(len(noisy[pair]), []).append(j)
+    for L, js in by_len.items():
+        pairs = sorted({specs[ids[j]][0] for j in js})
+        slot = {p: s for s, p in enumerate(pairs)}
+        nz = torch.as_tensor(np.stack([np.asarray(noisy[p], np.float64) for p in pairs])).cuda()
+        cl = torch.as_tensor(np.stack([np.asarray(clean[p], np.float64) for p in pairs])).cuda()
+        sub = [(slot[specs[ids[j]][0]], specs[ids[j]][1], specs[ids[j]][2]) for j in js]
+        res = eng.run(nz, sub, clean=cl)
+        cpow = (cl ** 2).sum(dim=1).cpu().numpy()
+        snr = snr_db(res["sse"], cpow[[s for (s, _, _) in sub]])
+        out[js, 0] = res["sse"]
+        out[js, 1] = snr
+        out[js, 2] = res["finite"]
+    return out
+
+
+def gather_records(local, n_total, group=None, device=None):
+    """All-gather per-cell records [n_local, 4] (cell_id, sse, snr, finite)
+    from every rank into one [n_total, 3] table indexed by cell_id.  Fixed-size
+    rows padded to the largest shard so one all_gather_into_tensor moves them."""
+    import torch
+    import torch.distributed as dist
+    if group is None and not (dist.is_available() and dist.is_initialized()):
+        world = 1
+    else:
+        world = dist.get_world_size(group)
+    rec = torch.as_tensor(np.asarray(local, dtype=np.float64).reshape(-1, 4))
+    if world > 1:
+        n = torch.tensor([rec.shape[0]], dtype=torch.int64, device=device)
+        counts = torch.zeros(world, dtype=torch.int64, device=device)
+        dist.all_gather_into_tensor(counts, n, group=group)
+        m = int(counts.max())
+        pad = torch.full((m, 4), -1.0, dtype=torch.float64)
+        pad[:rec.shape[0]] = rec
+        pad = pad.to(device) if device is not None else pad
+        allrec = torch.empty((world * m, 4), dtype=torch.float64, device=pad.device)
+        dist.all_gather_into_tensor(allrec, pad, group=group)
+        rec = allrec.cpu()
+    rec = rec.numpy()
+    rec = rec[rec[:, 0] >= 0]
+    table = np.full((n_total, 3), np.nan)
+    ids = rec[:, 0].astype(np.int64)
+    if len(np.unique(ids)) != len(ids) or len(ids) != n_total:
+        raise RuntimeError(f"gather: {len(ids)} records for {n_total} cells "
+                           f"({len(ids) - len(np.unique(ids))} duplicates)")
+    table[ids] = rec[:, 1:]
+    return table
+
+
+def select_best(specs, table, objective="snr", tol=None):
+    """Per (pair, algorithm): the winner of the reference's sequential scan.
+
+    Non-finite cells are skipped like finalize_enhanced returning None
+    (speech_enhancement_comparison.py:102-103,173-175); the incumbent starts
+    at -1 (:126-141).  Returns {(pair, alg): (cell_id or -1, score)}."""
+    tol = TOLERANCE[objective] if tol is None else tol
+    col = {"snr": 1}[objective]
+    groups = OrderedDict()
+    for cid, (pair, alg, _) in enumerate(specs):
+        groups.setdefault((pair, alg), []).append(cid)
+    best = OrderedDict()
+    for key, ids in groups.items():
+        incumbent, win = -1.0, -1
+        for cid in ids:
+            if not table[cid, 2]:
+                continue
+            s = table[cid, col]
+            if s > incumbent + tol:
+                incumbent, win = s, cid
+        best[key] = (win, incumbent if win >= 0 else None)
+    return best
+
+
+def run_grid(clean, noisy, specs, compute=None, group=None, device=None, objective="snr"):
+    """Run every cell of ``specs`` across the ranks of ``group`` (or locally)
+    and return (table [n_cells, 3] = sse, snr, finite, winners).  Every rank
+    gets the full table (all_gather); the selection is the deterministic
+    sequential scan, identical on every rank."""
+    import torch.distributed as dist
+    dist_on = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if dist_on else 1
+    rank = dist.get_rank(group) if dist_on else 0
+    lengths = [len(x) for x in noisy]
+    rank_of, _ = assign_lpt(specs, lengths, world)
+    ids = np.nonzero(rank_of == rank)[0]
+    compute = compute or engine_compute
+    vals = compute(clean, noisy, specs, ids) if len(ids) else np.zeros((0, 3))
+    local = np.concatenate([ids[:, None].astype(np.float64), vals], axis=1)
+    table = gather_records(local, len(specs), group=group, device=device)
+    return table, select_best(specs, table, objective)
+
+
+def optimize_parameters(clean_reference, noisy_audio, sr, algorithm, param_ranges=None,
+                        compute=None):
+    """Single-pair, single-algorithm mirror of the reference's
+    optimize_parameters (speech_enhancement_comparison.py:108-263) scored by
+    SNR: returns {'snr': {'score', 'params', 'cell'}, 'baseline': {'snr'},
+    'improvements': {'snr'}}; raises ValueError like :251-253 when no cell
+    produced a finite output."""
+    from .engine import canonical_algo
+    if sr != 16000:
+        raise ValueError("the device path runs at 16 kHz (prepare_pair resamples to 16 kHz)")
+    alg = canonical_algo(algorithm)
+    grids = {alg: param_ranges or ALGORITHM_GRIDS[alg]}
+    specs = job_specs(1, [alg], grids)
+    clean = [np.asarray(clean_reference, np.float64)]
+    noisy = [np.asarray(noisy_audio, np.float64)]
+    table, best = run_grid(clean, noisy, specs, compute=compute)
+    cid, score = best[(0, alg)]
+    if cid < 0:
+        raise ValueError("Optimization failed for snr - no valid parameters found!")
+    c, n = clean[0], noisy[0]
+    m = min(len(c), len(n))
+    err = np.sum((c[:m] - n[:m]) ** 2)
+    base = math.inf if err == 0 else float(10 * np.log10(np.sum(c[:m] ** 2) / (err + 1e-10)))
+    return {"snr": {"score": score, "params": dict(specs[cid][2]), "cell": int(cid)},
+            "baseline": {"snr": base}, "improvements": {"snr": score - base},
+            "table": table}

@@ -1,0 +1,65 @@
+"""Helpers for the multi-process grid tests (CPU, gloo): an oracle-backed
+compute function standing in for the device engine, and the rank entry point.
+Test infrastructure only."""
+
+import os
+
+import numpy as np
+
+SMALL_GRIDS = {
+    "spectralSubtractor": {"alpha": [1.0, 2.0], "beta": [0.01, 0.1], "n_fft": [512],
+                           "hop_length": [128, 256], "noise_percentile": [10.0],
+                           "noise_method": ["percentile", "min_tracking"]},
+    "mmse": {"alpha": [0.95], "ksi_min": [0.01, 0.1], "gain_min": [0.05], "gain_max": [1.0],
+             "n_fft": [512], "hop_length": [128], "noise_percentile": [10.0, 20.0],
+             "noise_method": ["percentile", "min_tracking"]},
+    "wiener": {"alpha": [0.9, 0.98], "gain_floor": [0.05], "n_fft": [512, 1024],
+               "hop_length": [256], "noise_percentile": [20.0], "noise_method": ["percentile"]},
+    "omlsa": {"alpha": [0.9], "ksi_min": [0.01], "gain_floor": [0.1], "noise_mu": [0.95],
+              "q": [0.3, 0.5], "n_fft": [512], "hop_length": [128],
+              "noise_percentile": [10.0], "noise_method": ["percentile", "min_tracking"]},
+}
+
+
+def pairs(n=3, seconds=0.3):
+    from classical_speech_enhancement_amd.synth import make_pair
+    out = [make_pair(i, seconds) for i in range(n)]
+    return [c for c, _ in out], [x for _, x in out]
+
+
+def oracle_compute(clean, noisy, specs, ids):
+    """Per-cell (sse, snr, finite) from the CPU oracle at lag 0."""
+    import oracle
+    out = np.zeros((len(ids), 3))
+    for j, cid in enumerate(ids):
+        pair, alg, p = specs[cid]
+        kw = dict(p)
+        if kw["noise_method"] == "true_noise":
+            kw["clean_audio"] = clean[pair]
+        y = oracle.ALGORITHMS[alg](noisy[pair], 16000, **kw)
+        fin = bool(np.all(np.isfinite(y)))
+        e = np.clip(y, -1.0, 1.0)
+        c = np.asarray(clean[pair], np.float64)
+        out[j] = (np.sum((c - e) ** 2), oracle.calculate_snr(c, e), fin)
+    return out
+
+
+def rank_main(rank, world, port, outdir):
+    import torch.distributed as dist
+    from classical_speech_enhancement_amd import search
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        clean, noisy = pairs()
+        specs = search.job_specs(len(noisy), grids=SMALL_GRIDS)
+        calls = []
+
+        def compute(c, n, s, ids):
+            calls.append(list(map(int, ids)))
+            return oracle_compute(c, n, s, ids)
+        table, best = search.run_grid(clean, noisy, specs, compute=compute)
+        win = np.array([[k[0], list(SMALL_GRIDS).index(k[1]), v[0]] for k, v in best.items()])
+        np.savez(os.path.join(outdir, f"rank{rank}.npz"), table=table, win=win,
+                 ids=np.array(calls[0] if calls else [], dtype=np.int64))
+    finally:
+        dist.destroy_process_group()
