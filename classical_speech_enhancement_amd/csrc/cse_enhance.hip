@@ -55,12 +55,40 @@ struct Args {
 // ---------------------------------------------------------------------------
 // special functions (fp32), coefficients from tools/gen_special.py
 // ---------------------------------------------------------------------------
+// Estrin's scheme: E(c[lo, lo+n)) = E(c[lo, lo+h)) + t^h E(c[lo+h, lo+n)), h the
+// largest power of two < n.  Depth ~log2(n) instead of Horner's n dependent
+// FMAs (the gain chains are latency-bound at 3 waves/SIMD); tools/gen_special.py
+// checks exactly this evaluation order in fp32.
+template <int LO, int N, int K, int NP>
+__device__ __forceinline__ float estrin_rec(const float (&c)[K], const float (&pw)[NP]) {
+    if constexpr (N == 1) {
+        return c[LO];
+    } else if constexpr (N == 2) {
+        return fmaf(c[LO + 1], pw[0], c[LO]);
+    } else {
+        constexpr int LH = 31 - __builtin_clz(N - 1);  // log2 of the largest power of two < N
+        constexpr int H = 1 << LH;
+        return fmaf(estrin_rec<LO + H, N - H>(c, pw), pw[LH], estrin_rec<LO, H>(c, pw));
+    }
+}
+
+#ifndef CSE_ESTRIN
+#define CSE_ESTRIN 0
+#endif
 template <int N>
 __device__ __forceinline__ float horner(const float (&c)[N], float t) {
-    float acc = c[N - 1];
+    if constexpr (!CSE_ESTRIN) {
+        float acc = c[N - 1];
 #pragma unroll
-    for (int k = N - 2; k >= 0; --k) acc = fmaf(acc, t, c[k]);
-    return acc;
+        for (int k = N - 2; k >= 0; --k) acc = fmaf(acc, t, c[k]);
+        return acc;
+    }
+    constexpr int NP = 32 - __builtin_clz(N - 1);  // powers t, t^2, ..., t^(2^(NP-1))
+    float pw[NP];
+    pw[0] = t;
+#pragma unroll
+    for (int k = 1; k < NP; ++k) pw[k] = pw[k - 1] * pw[k - 1];
+    return estrin_rec<0, N>(c, pw);
 }
 
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
@@ -110,8 +138,8 @@ __device__ __forceinline__ float gain_mmse(float P, float inv, float& rr, float 
     const float sv = __builtin_amdgcn_sqrtf(v);
     const float h = mmse_bracket(v, sv);
     float g = (0.88622692545275801f * (sv * fast_rcp(gam + 1e-12f))) * h;
-    if (__builtin_isnan(g)) g = gmin;
-    if (__builtin_isinf(g)) g = g > 0.0f ? gmax : gmin;
+    // nan_to_num(nan -> gmin, +inf -> gmax, -inf -> gmin) + clip (mmse.py:98-104):
+    // fmaxf returns the non-NaN operand, so the clip alone does all of it.
     g = fminf(fmaxf(g, gmin), gmax);
     rr = (g * g) * gam;
     return g;
@@ -134,9 +162,12 @@ __device__ __forceinline__ float gain_omlsa(float P, float inv, float& rr, float
     const float vc = fminf(v, CSE_EIN_VMAX);
     const float ein = horner(CSE_EINP, vc * (2.0f / CSE_EIN_VMAX) - 1.0f);
     const float X = xi * r * (small ? __builtin_amdgcn_rsqf(vc) : 1.0f);
-    float lg = fast_log2(X) + (small ? (0.5f * kLog2e) * (ein - 0.5772156649015329f) : 0.0f);
-    if (__builtin_isnan(lg)) lg = lg2_floor;          // nan_to_num(nan -> gain_floor)
-    if (__builtin_isinf(lg)) lg = lg > 0.0f ? 0.0f : lg2_floor;
+    // nan_to_num of g_lsa (advanced_mmse.py:106) needs no code: for finite
+    // input 0 <= X <= 1e6, so lg is finite or -inf (xi = 0 with ksi_min = 0),
+    // and -inf gives g = exp2(-inf) = 0 -> clip -> gain_floor, the reference's
+    // 0**p * gf**(1-p) clipped (p >= 1e-10 > 0).  Non-finite input makes the
+    // cell non-finite either way.
+    const float lg = fast_log2(X) + (small ? (0.5f * kLog2e) * (ein - 0.5772156649015329f) : 0.0f);
     const float ev = fast_exp2(v * kLog2e);
     const float A = q * (r * ev) + 1e-10f;
     const float p = fminf(fmaxf(A * fast_rcp(A + (1.0f - q)), 0.0f), 1.0f);
