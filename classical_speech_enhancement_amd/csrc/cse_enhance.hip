@@ -72,6 +72,11 @@ __device__ __forceinline__ float estrin_rec(const float (&c)[K], const float (&p
     }
 }
 
+#ifdef CSE_MARKS  // static instruction-count analysis builds only (tools/isa_sections.py)
+#define CSE_MARK(name) asm volatile(";#MARK " name)
+#else
+#define CSE_MARK(name)
+#endif
 #ifndef CSE_ESTRIN
 #define CSE_ESTRIN 0
 #endif
@@ -303,6 +308,38 @@ __device__ __forceinline__ cf gain_bin(float2 y, float nz, float& rr, float alph
     return cmk(y.x * g, y.y * g);
 }
 
+// One frame's gain stage for one lane: bins i + L*j (j < 16) and, on lane 0,
+// the Nyquist bin M.  The row pointers are __restrict__ (the Y/N rows and the
+// cell's S row are disjoint LDS ranges), so after inlining the scheduler may
+// issue all 17 bins' reads up front and interleave the 17 independent gain
+// chains instead of serialising read -> gain -> write per bin.  Lanes other
+// than 0 compute a throw-away 17th bin from in-bounds LDS (the row after Y/N)
+// rather than branching: a masked branch costs the wave the same issue slots.
+template <int NFFT, int ALGO, bool OUT>
+__device__ __forceinline__ void gain_row(const float2* __restrict__ yr, const float* __restrict__ nr,
+                                         cf* __restrict__ sb, float (&rr)[17], float alpha_t,
+                                         const CellParam& cpar, float* __restrict__ grow, int i) {
+    constexpr int L = Geo<NFFT>::L, M = Geo<NFFT>::M;
+    float2 y[17];
+    float n[17];
+#pragma unroll
+    for (int j = 0; j < 17; ++j) {
+        const int kk = (j < 16) ? L * j : M;  // k - i
+        y[j] = yr[kk];
+        n[j] = nr[kk];
+    }
+#pragma unroll
+    for (int j = 0; j < 17; ++j) {
+        const int kk = (j < 16) ? L * j : M;
+        float g;
+        const cf Sj = gain_bin<ALGO>(y[j], n[j], rr[j], alpha_t, cpar, g);
+        if (j < 16 || i == 0) {
+            sb[kk] = Sj;
+            if (OUT && grow) grow[kk] = g;
+        }
+    }
+}
+
 template <int NFFT, int HOP, int ALGO, bool OUT>
 __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, int n_cells_wg,
                                        unsigned char* smem) {
@@ -453,6 +490,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             // the one workgroup barrier per frame: rows(t) (stored during frame
             // t-1) are visible, and nobody still reads buffer (t+1)&1
             if (!(CSE_ABLATE & 8)) __syncthreads();
+            CSE_MARK("gain");
             // ---------------- gain stage: S = Y * G into my cell's LDS row
             {
                 const CellParam cpar =
@@ -463,29 +501,15 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     (const float2*)(smem + opaque(W::OFF_Y + (t & 1) * W::YROW + 8 * i));
                 const float* nr =
                     (const float*)(smem + opaque(W::OFF_N + (t & 1) * W::NROW + 4 * i));
-                float2 y_nx = yr[0];
-                float n_nx = nr[0];
-#pragma unroll
-                for (int j = 0; j < 17; ++j) {
-                    const int kk = (j < 16) ? L * j : M;  // k - i
-                    const float2 y = y_nx;
-                    const float nz = n_nx;
-                    if (j < 16) {  // prefetch the next bin's row entries
-                        const int kn = (j + 1 < 16) ? L * (j + 1) : M;
-                        y_nx = yr[kn];
-                        n_nx = nr[kn];
-                    }
-                    if (j == 16 && i != 0) break;
-                    float g;
-                    const cf Sj = gain_bin<ALGO>(y, nz, rr[j], alpha_t, cpar, g);
-                    sb[kk] = Sj;
-                    if (OUT && gout) gout[t * B + i + kk] = g;
-                }
+                gain_row<NFFT, ALGO, OUT>(yr, nr, sb, rr, alpha_t, cpar,
+                                          (OUT && gout) ? gout + t * B + i : nullptr, i);
             }
+            CSE_MARK("rows");
             store_rows(t + 1);  // other buffer: its last readers passed this frame's barrier
             load_rows(t + 2);
             wave_sync();  // my wave's S rows complete (cells never span waves)
 
+            CSE_MARK("pass1");
             // ---------------- pass 1: real-IFFT packing + DFT16 over j -----
             // Z'[k] = (X_k + X*_{M-k}) + i (X_k - X*_{M-k}) e^{2πi k/NFFT}
             cf z[16];
@@ -521,6 +545,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             }
             wave_sync();  // transpose block written
 
+            CSE_MARK("pass2");
             // ---------------- pass 2: DFT over the lane index --------------
             cf v[16];
             {
@@ -539,6 +564,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 }
             }
             if (!(CSE_ABLATE & 2)) idft16(v);
+            CSE_MARK("window");
             // ---------------- synthesis window (/n_fft) --------------------
             {
                 const LaneConst lc = *(const LaneConst*)(smem + opaque(W::OFF_LC + 48 * i));
@@ -554,6 +580,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             for (int q = 0; q < 32; ++q) x[q] = 0.0f;
         }
 
+        CSE_MARK("retire");
         // ---------------- overlap-add + retire HOP finished samples ---------
         // slot q < F of this frame completes output position t*HOP + n(q):
         // y = (ola) / wss (librosa istft normalisation), then the SNR error
@@ -610,6 +637,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 #pragma unroll
             for (int q = 0; q < F; ++q) asm volatile("" ::"v"(done[q]));
         }
+        CSE_MARK("end");
     }
 
     // ---------------- per-cell reductions over the cell's L lanes ----------
