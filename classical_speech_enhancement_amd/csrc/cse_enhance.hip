@@ -219,9 +219,17 @@ struct WG {
     static constexpr int OFF_N = OFF_Y + 2 * YROW;                // float[2][B]
     static constexpr int OFF_C = OFF_N + 2 * NROW;                // float[2][HMAX]
     static constexpr int OFF_TW = OFF_C + 2 * HMAX * 4;           // cf[15][L] (b = 1..15)
-    static constexpr int OFF_LC = OFF_TW + 15 * G::L * 8;         // float[L][12] lane constants
-    static constexpr int OFF_CP = OFF_LC + G::L * 48;             // float[CPWG][8] cell params
-    static constexpr int BYTES = OFF_CP + CPWG * 32;
+    static constexpr int OFF_LC = OFF_TW + 15 * G::L * 8;         // cf[L] packing rotor
+    static constexpr int OFF_CP = OFF_LC + G::L * 8;              // float[CPWG][8] cell params
+    // synthesis window w(n)/NFFT at the lane's 32 sample slots; row stride 36
+    // floats (144 B = 36 banks): the 16 lanes' ds_read_b128 hit disjoint banks
+    static constexpr int WSTR = 36;
+    static constexpr int OFF_WIN = OFF_CP + CPWG * 32;
+    // 1/wss at the lane's 16 retired slots, only for the one R = 2 case
+    // (512/256), whose wss is not constant; row stride 20 floats (disjoint banks)
+    static constexpr int ISTR = 20;
+    static constexpr int OFF_IWS = OFF_WIN + G::L * WSTR * 4;
+    static constexpr int BYTES = OFF_IWS + (NFFT == 512 ? G::L * ISTR * 4 : 0);
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
@@ -257,23 +265,6 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// lane constants (depend only on the lane-in-cell i), kept in LDS so they do
-// not occupy VGPRs across the frame loop: the packing rotor e^{2πi i/NFFT},
-// the window phase (pre-scaled by 0.5/NFFT) of the lane's two sample parities,
-// and the 512/256 closed-form wss phase.
-struct LaneConst {
-    float bc, bs, wc0, wc1, ws0, ws1, pc0, pc1, ps0, ps1, pad0, pad1;
-};
-static_assert(sizeof(LaneConst) == 48, "LaneConst layout");
-
-template <int NFFT>
-__device__ __forceinline__ float hann_at(int aidx, int e, const LaneConst& lc) {
-    // w(n)/NFFT at n = SP*aidx + off + e
-    const float ca = Rot32::c[(2 * aidx) & 31], sa = Rot32::s[(2 * aidx) & 31];
-    const float wc = e ? lc.wc1 : lc.wc0, ws = e ? lc.ws1 : lc.ws0;
-    return 0.5f / NFFT - (ca * wc - sa * ws);
 }
 
 // per-cell parameters as the gain stage wants them
@@ -386,22 +377,23 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         sincospi(2.0 * (double)(ii * b) / (double)M, &s, &c);
         ((cf*)(smem + W::OFF_TW))[e] = cmk((float)c, (float)s);
     }
-    for (int ii = tid; ii < L; ii += W::THREADS) {
-        LaneConst lc;
+    // lane tables: packing rotor e^{2πi ii/NFFT}; window w(n)/NFFT at the
+    // lane's sample slots q (n = SP*(q>>1) + off + (q&1)); for 512/256 the
+    // reciprocal closed-form wss 0.75 + 0.25 cos(2π n/256) at its retired slots
+    for (int e = tid; e < L * 32; e += W::THREADS) {
+        const int ii = e / 32, q = e % 32;
         const int bb = (L == 16) ? ii : (ii & 15), hh = (L == 16) ? 0 : (ii >> 4);
-        const int of = 2 * bb + 32 * hh;
-        sincospif(2.0f * (float)ii / (float)NFFT, &lc.bs, &lc.bc);
-        float s_, c_;
-        sincospif(2.0f * (float)of / (float)NFFT, &s_, &c_);
-        lc.wc0 = (0.5f / NFFT) * c_;
-        lc.ws0 = (0.5f / NFFT) * s_;
-        sincospif(2.0f * (float)(of + 1) / (float)NFFT, &s_, &c_);
-        lc.wc1 = (0.5f / NFFT) * c_;
-        lc.ws1 = (0.5f / NFFT) * s_;
-        sincospif(2.0f * (float)of / 256.0f, &lc.ps0, &lc.pc0);
-        sincospif(2.0f * (float)(of + 1) / 256.0f, &lc.ps1, &lc.pc1);
-        lc.pad0 = lc.pad1 = 0.0f;
-        ((LaneConst*)(smem + W::OFF_LC))[ii] = lc;
+        const int n = SP * (q >> 1) + 2 * bb + 32 * hh + (q & 1);
+        const double w = 0.5 - 0.5 * cospi(2.0 * (double)n / (double)NFFT);
+        ((float*)(smem + W::OFF_WIN))[ii * W::WSTR + q] = (float)(w / NFFT);
+        if (NFFT == 512 && HOP == 256 && q < 16)
+            ((float*)(smem + W::OFF_IWS))[ii * W::ISTR + q] =
+                (float)(1.0 / (0.75 + 0.25 * cospi(2.0 * (double)n / 256.0)));
+        if (q == 0) {
+            double sn, cs;
+            sincospi(2.0 * (double)ii / (double)NFFT, &sn, &cs);
+            ((cf*)(smem + W::OFF_LC))[ii] = cmk((float)cs, (float)sn);
+        }
     }
     for (int c = tid; c < W::CPWG; c += W::THREADS) {
         const cse_cell_t* cp = wcell + (c < n_cells_wg ? c : 0);
@@ -482,7 +474,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 #pragma unroll
     for (int q = 0; q < PEND; ++q) acc[q] = 0.0f;
     double sse = 0.0;
-    bool fin = true;
+    float chk = 0.0f;  // sum of y*0 over retired samples: NaN iff some y is not finite
 
     for (int t = 0; t < nf + R - 1; ++t) {
         float x[32];  // this frame's windowed IFFT samples (0 in flush frames)
@@ -514,8 +506,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             // Z'[k] = (X_k + X*_{M-k}) + i (X_k - X*_{M-k}) e^{2πi k/NFFT}
             cf z[16];
             {
-                const LaneConst* lcp = (const LaneConst*)(smem + opaque(W::OFF_LC + 48 * i));
-                const cf base = cmk(lcp->bc, lcp->bs);
+                const cf base = *(const cf*)(smem + opaque(W::OFF_LC + 8 * i));
                 const cf* sa = (const cf*)(smem + opaque(creg + 8 * i));                   // S[i + L j]
                 const cf* sm = (const cf*)(smem + opaque(creg + 8 * (M - i - 15 * L)));   // S[M - i - L j]
 #pragma unroll
@@ -567,10 +558,9 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             CSE_MARK("window");
             // ---------------- synthesis window (/n_fft) --------------------
             {
-                const LaneConst lc = *(const LaneConst*)(smem + opaque(W::OFF_LC + 48 * i));
+                const float* wt = (const float*)(smem + opaque(W::OFF_WIN + 4 * W::WSTR * i));
 #pragma unroll
-                for (int q = 0; q < 32; ++q)
-                    x[q] = ((q & 1) ? v[q >> 1].y : v[q >> 1].x) * hann_at<NFFT>(q >> 1, q & 1, lc);
+                for (int q = 0; q < 32; ++q) x[q] = ((q & 1) ? v[q >> 1].y : v[q >> 1].x) * wt[q];
             }
         } else {
             __syncthreads();  // flush frames: clean row t visible, row t-1 reads done
@@ -593,43 +583,60 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 #pragma unroll
         for (int q = 0; q < PEND; ++q) acc[q] = (q + F < PEND ? acc[q + F] : 0.0f) + x[q + F];
         if (valid && !(CSE_ABLATE & 4)) {
-            const LaneConst lc = *(const LaneConst*)(smem + opaque(W::OFF_LC + 48 * i));
-            const bool edge = (t < R - 1) || (t >= nf);
             const int o0 = t * HOP + off - NFFT / 2;  // output index of q = 0
             const float* crow_t = (const float*)(smem + opaque(W::OFF_C + (t & 1) * W::HMAX * 4 +
                                                                4 * off));
+            // frame t retires output positions [t*HOP - NFFT/2, (t+1)*HOP - NFFT/2)
+            const bool edge = (t < R - 1) || (t >= nf);
+            const bool interior = !edge && (t + 1) * HOP - NFFT / 2 <= len;  // uniform
+            float inv[F];
+            if (R == 2) {
+                const float* it = (const float*)(smem + opaque(W::OFF_IWS + 4 * W::ISTR * i));
+#pragma unroll
+                for (int q = 0; q < F; ++q) inv[q] = it[q];
+            } else {
+#pragma unroll
+                for (int q = 0; q < F; ++q) inv[q] = (R == 4) ? (1.0f / 1.5f) : (1.0f / 3.0f);
+            }
             float part = 0.0f;
+            if (interior) {
+                // steady state: every slot is inside [0, len); the finiteness
+                // check rides along as chk += y*0 (NaN for a NaN or inf y)
 #pragma unroll
-            for (int q = 0; q < F; ++q) {
-                const int n = SP * (q >> 1) + (q & 1);  // + off: position inside frame t
-                const int o = o0 + n;
-                float inv;
-                if (R == 2) {  // 0.75 + 0.25 cos(2π n/256) for 512/256; n = 32 aq + off + e
-                    const int m = (4 * (q >> 1)) & 31;
-                    inv = __builtin_amdgcn_rcpf(
-                        0.75f + 0.25f * (Rot32::c[m] * ((q & 1) ? lc.pc1 : lc.pc0) -
-                                         Rot32::s[m] * ((q & 1) ? lc.ps1 : lc.ps0)));
-                } else {
-                    inv = (R == 4) ? (1.0f / 1.5f) : (1.0f / 3.0f);
-                }
-                if (edge) {
-                    float wss = 0.0f;
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const int tr = t - r;
-                        if (tr >= 0 && tr < nf) {
-                            const float w = hann_at<NFFT>((q >> 1) + r * (HOP / SP), q & 1, lc) * NFFT;
-                            wss = fmaf(w, w, wss);
-                        }
-                    }
-                    inv = wss > 0.0f ? __builtin_amdgcn_rcpf(wss) : 1.0f;
-                }
-                if (o >= 0 && o < len) {
-                    const float y = done[q] * inv;
-                    fin = fin && __builtin_isfinite(y);
-                    if (OUT && yout) yout[o] = y;
+                for (int q = 0; q < F; ++q) {
+                    const int n = SP * (q >> 1) + (q & 1);
+                    const float y = done[q] * inv[q];
+                    chk = fmaf(y, 0.0f, chk);
+                    if (OUT && yout) yout[o0 + n] = y;
                     const float d = crow_t[n] - fminf(fmaxf(y, -1.0f), 1.0f);
                     part = fmaf(d, d, part);
+                }
+            } else {
+                const float* wt = (const float*)(smem + opaque(W::OFF_WIN + 4 * W::WSTR * i));
+#pragma unroll
+                for (int q = 0; q < F; ++q) {
+                    const int n = SP * (q >> 1) + (q & 1);  // + off: position inside frame t
+                    const int o = o0 + n;
+                    float iv = inv[q];
+                    if (edge) {  // sum the windows of the frames that cover this sample
+                        float wss = 0.0f;
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const int tr = t - r;
+                            if (tr >= 0 && tr < nf) {
+                                const float w = wt[q + 2 * r * (HOP / SP)] * NFFT;
+                                wss = fmaf(w, w, wss);
+                            }
+                        }
+                        iv = wss > 0.0f ? __builtin_amdgcn_rcpf(wss) : 1.0f;
+                    }
+                    if (o >= 0 && o < len) {
+                        const float y = done[q] * iv;
+                        chk = fmaf(y, 0.0f, chk);
+                        if (OUT && yout) yout[o] = y;
+                        const float d = crow_t[n] - fminf(fmaxf(y, -1.0f), 1.0f);
+                        part = fmaf(d, d, part);
+                    }
                 }
             }
             sse += (double)part;
@@ -643,7 +650,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     // ---------------- per-cell reductions over the cell's L lanes ----------
 #pragma unroll
     for (int m = L / 2; m > 0; m >>= 1) sse += __shfl_xor(sse, m, 64);
-    const unsigned long long bad = __ballot(!fin);
+    const unsigned long long bad = __ballot(chk != 0.0f);  // NaN != 0
     const unsigned long long my = (bad >> (cs * L)) & ((1ull << L) - 1);
     const int64_t cell_idx = (int64_t)(wcell - a.cells) + cslot;
     if (i == 0 && valid) {
