@@ -139,7 +139,7 @@ __device__ __forceinline__ float gain_mmse(float P, float inv, float& rr, float 
                                            float ksi_min, float gmin, float gmax) {
     const float gam = fmaxf(P * inv, 1e-12f);
     const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * fmaxf(gam - 1.0f, 0.0f), ksi_min);
-    const float v = fminf(fmaxf(xi * gam * fast_rcp(1.0f + xi), 1e-12f), 80.0f);
+    const float v = __builtin_amdgcn_fmed3f(xi * gam * fast_rcp(1.0f + xi), 1e-12f, 80.0f);
     const float sv = __builtin_amdgcn_sqrtf(v);
     const float h = mmse_bracket(v, sv);
     float g = (0.88622692545275801f * (sv * fast_rcp(gam + 1e-12f))) * h;
@@ -151,33 +151,32 @@ __device__ __forceinline__ float gain_mmse(float P, float inv, float& rr, float 
 }
 
 // Log-MMSE x speech-presence gain (advanced_mmse.py:100-121), in the log2 domain:
-//   log2 g_lsa = log2(xi/(1+xi)) + 0.5 log2(e) E1(v),  E1 = Ein(v) - ln v - gamma_E
-//             = log2(xi r / sqrt(v)) + 0.5 log2(e) (Ein(v) - gamma_E)      (v < 17)
-//             = log2(xi r)                                               (v >= 17: E1 < 2.4e-9)
+//   log2 g_lsa = log2(xi/(1+xi)) + 0.5 log2(e) E1(v)
+//             = log2(xi r / sqrt(vc)) + Q(vc),  vc = min(v, 11)
+//   with Q = 0.5 log2(e) (Ein - gamma_E) (tools/gen_special.py); for v >= 11 this
+//   differs from the exact form by 0.5 log2(e)(E1(11) - E1(v)) < 1.1e-6, no branch.
 //   p = 1/(1 + (1-q)/(q Lambda + eps)) = A / (A + 1 - q),  A = q Lambda + eps
 //   G = clip(g_lsa^p gf^(1-p), gf, 1) = clip(exp2(lgf + p (lg - lgf)), gf, 1)
+// nan_to_num of g_lsa (advanced_mmse.py:106) needs no code: for finite input
+// 0 <= X <= 1e6, so lg is finite or -inf (xi = 0 with ksi_min = 0), and -inf
+// gives g = exp2(-inf) = 0 -> clip -> gain_floor, the reference's 0**p * gf**(1-p)
+// clipped (p >= 1e-10 > 0).  Non-finite input makes the cell non-finite either way.
 __device__ __forceinline__ float gain_omlsa(float P, float inv, float& rr, float alpha_t,
                                             float ksi_min, float gfloor, float lg2_floor, float q,
                                             float vmax) {
     const float gam = fmaxf(P * inv, 1e-10f);
     const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * fmaxf(gam - 1.0f, 0.0f), ksi_min);
     const float r = fast_rcp(1.0f + xi);
-    const float v = fminf(fmaxf(xi * gam * r, 1e-12f), vmax);
-    const bool small = v < CSE_EIN_VMAX;
-    const float vc = fminf(v, CSE_EIN_VMAX);
-    const float ein = horner(CSE_EINP, vc * (2.0f / CSE_EIN_VMAX) - 1.0f);
-    const float X = xi * r * (small ? __builtin_amdgcn_rsqf(vc) : 1.0f);
-    // nan_to_num of g_lsa (advanced_mmse.py:106) needs no code: for finite
-    // input 0 <= X <= 1e6, so lg is finite or -inf (xi = 0 with ksi_min = 0),
-    // and -inf gives g = exp2(-inf) = 0 -> clip -> gain_floor, the reference's
-    // 0**p * gf**(1-p) clipped (p >= 1e-10 > 0).  Non-finite input makes the
-    // cell non-finite either way.
-    const float lg = fast_log2(X) + (small ? (0.5f * kLog2e) * (ein - 0.5772156649015329f) : 0.0f);
+    const float xr = xi * r;
+    const float v = __builtin_amdgcn_fmed3f(xr * gam, 1e-12f, vmax);
+    const float vc = fminf(v, CSE_LSA_VMAX);
+    const float Q = horner(CSE_LSAQ, fmaf(vc, 2.0f / CSE_LSA_VMAX, -1.0f));
+    const float lg = fast_log2(xr * __builtin_amdgcn_rsqf(vc)) + Q;
     const float ev = fast_exp2(v * kLog2e);
     const float A = q * (r * ev) + 1e-10f;
     const float p = fminf(fmaxf(A * fast_rcp(A + (1.0f - q)), 0.0f), 1.0f);
     const float g = fast_exp2(lg2_floor + p * (lg - lg2_floor));
-    const float G = fminf(fmaxf(g, gfloor), 1.0f);
+    const float G = __builtin_amdgcn_fmed3f(g, gfloor, 1.0f);  // g >= 0, never NaN
     rr = (G * G) * gam;
     return G;
 }
