@@ -117,7 +117,11 @@ __device__ __forceinline__ void idft16(cf (&v)[16]) {
 #pragma unroll
     for (int n1 = 1; n1 < 4; ++n1)
 #pragma unroll
-        for (int k2 = 1; k2 < 4; ++k2) v[4 * n1 + k2] = cmul(v[4 * n1 + k2], w16(n1 * k2));
+        for (int k2 = 1; k2 < 4; ++k2) {
+            const int m = n1 * k2;
+            // W16^4 = i: a swap, not a multiply (a 0*x product does not fold under IEEE)
+            v[4 * n1 + k2] = (m == 4) ? cmuli(v[4 * n1 + k2]) : cmul(v[4 * n1 + k2], w16(m));
+        }
     // step 2: for each n1, DFT4 over k2 -> index n2; result x[n1 + 4n2]
 #pragma unroll
     for (int n1 = 0; n1 < 4; ++n1) idft4(v[4 * n1], v[4 * n1 + 1], v[4 * n1 + 2], v[4 * n1 + 3]);

@@ -508,6 +508,13 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 const cf base = *(const cf*)(smem + opaque(W::OFF_LC + 8 * i));
                 const cf* sa = (const cf*)(smem + opaque(creg + 8 * i));                   // S[i + L j]
                 const cf* sm = (const cf*)(smem + opaque(creg + 8 * (M - i - 15 * L)));   // S[M - i - L j]
+                // rotor tw_j = e^{2πi (i + L j)/NFFT} = base * W32^j; W32^8 = i gives
+                // tw_{j+8} = i tw_j, so only j < 8 is computed and, with
+                // P = D tw:  z_j = S + i P_j (j < 8),  z_{j+8} = S - P'_{j} (P' = D tw_j)
+                cf tw[8];
+                tw[0] = base;
+#pragma unroll
+                for (int j = 1; j < 8; ++j) tw[j] = cmul(base, cmk(Rot32::c[j], Rot32::s[j]));
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     cf A = sa[L * j];
@@ -516,9 +523,15 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                         A.y = 0.0f;
                         Bm.y = 0.0f;
                     }
-                    const cf Bc = cconj(Bm);
-                    const cf tw = cmul(base, cmk(Rot32::c[j], Rot32::s[j]));  // e^{2πi k/NFFT}
-                    z[j] = cadd(cadd(A, Bc), cmuli(cmul(csub(A, Bc), tw)));
+                    // S = A + conj(Bm), D = A - conj(Bm)
+                    const float sx = A.x + Bm.x, sy = A.y - Bm.y;
+                    const float dx = A.x - Bm.x, dy = A.y + Bm.y;
+                    const cf w = tw[j & 7];
+                    if (j < 8) {  // S + i (D w)
+                        z[j] = cmk(fmaf(-dx, w.y, fmaf(-dy, w.x, sx)), fmaf(dx, w.x, fmaf(-dy, w.y, sy)));
+                    } else {      // S + i (D i w) = S - D w
+                        z[j] = cmk(fmaf(-dx, w.x, fmaf(dy, w.y, sx)), fmaf(-dx, w.y, fmaf(-dy, w.x, sy)));
+                    }
                 }
             }
             if (!(CSE_ABLATE & 2)) idft16(z);
