@@ -284,10 +284,20 @@ __device__ __forceinline__ cf gain_bin(float2 y, float nz, float& rr, float alph
         // Ps = max(P - a N, b N); |S| = sqrt(Ps) with the noisy phase
         // (spectral_subtractor.py:44-53).  No eps floor: the reference floors
         // BEFORE fix_length (engine.noise_key).
+        // The raw v_sqrt/v_rsq treat denormal inputs as 0, and a near-silent
+        // clip (fix_length zero-pads N, so Ps = P) reaches them: sqrt is
+        // taken of a rescaled Ps below 2^-96, and the noisy phase y/|y| of a
+        // rescaled y below 2^-50.
         const float ps = fmaxf(P - cp.p0 * nz, cp.p1 * nz);
-        const float sp = __builtin_amdgcn_sqrtf(ps);
-        g = (P > 0.0f) ? sp * __builtin_amdgcn_rsqf(P) : 0.0f;
-        return (P > 0.0f) ? cmk(y.x * g, y.y * g) : cmk(sp, 0.0f);  // angle(0) = 0
+        const bool tiny_ps = ps < 0x1p-96f;
+        const float sp = __builtin_amdgcn_sqrtf(tiny_ps ? ps * 0x1p64f : ps) *
+                         (tiny_ps ? 0x1p-32f : 1.0f);
+        const float sc = fmaxf(fabsf(y.x), fabsf(y.y)) < 0x1p-50f ? 0x1p64f : 1.0f;
+        const float yx = y.x * sc, yy = y.y * sc;
+        const float pz = fmaf(yx, yx, yy * yy);
+        const float u = sp * __builtin_amdgcn_rsqf(pz);
+        g = (pz > 0.0f) ? u * sc : 0.0f;
+        return (pz > 0.0f) ? cmk(yx * u, yy * u) : cmk(sp, 0.0f);  // angle(0) = 0
     }
     if (ALGO == CSE_ALGO_WIENER)
         g = gain_wiener(P, nz, rr, alpha_t, cp.p1);

@@ -176,6 +176,30 @@ def gen_short(R):
     print("short done")
 
 
+def gen_tiny(R):
+    """Fixture 6: degenerate lengths — empty, single-sample, shorter than the
+    frame half-width (repeated reflect padding), one frame.  Errors the
+    reference raises are recorded as their exception class name."""
+    out = {}
+    for n in (0, 1, 2, 7, 100, 257, 700):
+        clean, noisy = make_pair(13, seconds=max(n, 1) / 16000.0)
+        noisy, clean = noisy[:n], clean[:n]
+        out[f"noisy|{n}"] = noisy
+        for alg, base in CELLS.items():
+            for method in ("percentile", "min_tracking"):
+                for n_fft, hop in ((512, 128), (1024, 256)):
+                    key = f"{n}|{alg}|{method}|{n_fft}|{hop}"
+                    try:
+                        y = R[alg](noisy, 16000, **dict(base, n_fft=n_fft, hop_length=hop,
+                                                        noise_percentile=20.0,
+                                                        noise_method=method))
+                        out["y|" + key] = np.asarray(y, dtype=np.float64)
+                    except Exception as e:  # noqa: BLE001 — the class is the fixture
+                        out["err|" + key] = np.array(type(e).__name__)
+    np.savez_compressed(os.path.join(OUT, "tiny_clips.npz"), **out)
+    print("tiny done", sum(k.startswith("err|") for k in out), "errors")
+
+
 def _read_wav(path):
     with wave.open(path) as w:
         assert w.getsampwidth() == 2 and w.getnchannels() == 1
@@ -228,7 +252,7 @@ def gen_presentation(R):
 
 if __name__ == "__main__":
     R = ref_modules()
-    which = sys.argv[1:] or ["algorithms", "config1", "short", "presentation", "grid"]
+    which = sys.argv[1:] or ["algorithms", "config1", "short", "presentation", "grid", "tiny"]
     if "algorithms" in which:
         gen_algorithms(R)
     if "config1" in which:
@@ -239,3 +263,5 @@ if __name__ == "__main__":
         gen_presentation(R)
     if "grid" in which:
         gen_grid_snr(R)
+    if "tiny" in which:
+        gen_tiny(R)

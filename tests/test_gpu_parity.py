@@ -32,6 +32,10 @@ def P():
     return plugins
 
 
+ORACLE = {"ss": oracle.spectral_subtraction, "wiener": oracle.wiener_filter,
+          "mmse": oracle.mmse, "omlsa": oracle.advanced_mmse}
+
+
 def _fn(P, alg):
     return {"ss": P.spectral_subtraction, "wiener": P.wiener_filter, "mmse": P.mmse,
             "omlsa": P.advanced_mmse}[alg]
@@ -90,6 +94,40 @@ def test_short_clip_edge_cases(P):
                                                      noise_percentile=20.0, noise_method=method))
                 ref = g[f"y|{tag}|{alg}|{method}"]
                 assert rel_l2(y, ref) <= TOL and rel_max(y, ref) <= TOL, (tag, alg, method)
+
+
+def test_tiny_lengths(P):
+    """1..700-sample inputs (repeated reflect padding, single frame) against the
+    reference fixture; the empty input raises ValueError."""
+    g = load_golden("tiny_clips.npz")
+    for key in g.files:
+        kind, rest = key.split("|", 1)
+        if kind not in ("y", "err"):
+            continue
+        n, alg, method, n_fft, hop = rest.split("|")
+        noisy = g[f"noisy|{n}"]
+        kw = dict(CELLS[alg], n_fft=int(n_fft), hop_length=int(hop), noise_percentile=20.0,
+                  noise_method=method)
+        if kind == "err":
+            with pytest.raises(ValueError):
+                _fn(P, alg)(noisy, 16000, **kw)
+            continue
+        y = _fn(P, alg)(noisy, 16000, **kw)
+        ref = g[key]
+        assert len(y) == len(ref)
+        assert np.all(np.isfinite(y)), key
+        # SS on 1-2 samples is ill-conditioned in the reference itself: its
+        # output is set by the phase of FFT rounding noise in the (exactly
+        # zero) bins above bin 1, because beta*N dominates there.  A 1e-9
+        # relative input perturbation moves the fp64 oracle by 40-70 %, so
+        # only finiteness and length are checked for such cases.
+        cond = rel_l2(ORACLE[alg](noisy * (1 + 1e-9), 16000, **kw), ref)
+        if cond > 1e-6:
+            continue
+        if np.max(np.abs(ref)) == 0:
+            assert np.max(np.abs(y)) == 0, key
+            continue
+        assert rel_l2(y, ref) <= TOL and rel_max(y, ref) <= TOL, (key, rel_l2(y, ref))
 
 
 def test_unknown_method_and_missing_clean_raise(P):
