@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """bench.py — STFT frame-gain evaluations/s on MI355X (BASELINE.json metric).
 
-Workload (one "step"): for P synthetic 10-s 16-kHz pairs per GPU, the n_fft=512
+Workload (one "step"): for P (default 13) synthetic 10-s 16-kHz pairs per GPU, the n_fft=512
 half of the reference's full HEAD grid (parameter_ranges.py: SS 360 + MMSE 960
 + Wiener 96 + OMLSA 3456 = 4872 cells per pair, hops 128 and 256):
   STFT + noise PSDs (percentile 10/20, min-tracking, smoothing)   [per pair]
@@ -120,7 +120,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs", type=int, default=8, help="10-s pairs per GPU")
+    ap.add_argument("--pairs", type=int, default=13,
+                    help="10-s pairs per GPU (13 x 8 GPUs = 104 >= the 100 pairs of config 4)")
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -132,8 +133,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
+        # "nccl" is RCCL on ROCm; CSE_DIST_BACKEND=gloo rehearses the
+        # multi-rank path with several ranks sharing one GPU (1-GPU boxes)
+        dist.init_process_group(os.environ.get("CSE_DIST_BACKEND", "nccl"))
+    torch.cuda.set_device(local % torch.cuda.device_count())
     from classical_speech_enhancement_amd.engine import Engine, snr_db
     from classical_speech_enhancement_amd.synth import make_pair
 
@@ -158,9 +161,12 @@ def main():
             ev[1].record()
         rec = torch.stack([plan.sse_d, plan.fin_d.double()])
         if world > 1:
-            out = torch.empty((world,) + rec.shape, dtype=rec.dtype, device=rec.device)
-            dist.all_gather_into_tensor(out, rec)
-            rec = out
+            if dist.get_backend() == "gloo":
+                rec = rec.cpu()
+            out = torch.empty((world * rec.shape[0],) + rec.shape[1:], dtype=rec.dtype,
+                              device=rec.device)
+            dist.all_gather_into_tensor(out, rec.contiguous())
+            rec = out.view((world,) + rec.shape)
         return rec.cpu()
 
     for _ in range(args.warmup):
@@ -179,7 +185,8 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64,
+                         device="cpu" if dist.get_backend() == "gloo" else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
