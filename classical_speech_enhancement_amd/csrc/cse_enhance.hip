@@ -239,7 +239,9 @@ static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
 
 // CSE_ABLATE (timing experiments only; 0 in every product build):
 //   1 = trivial gain (S = Y), 2 = no inverse FFT passes, 4 = no sample retire,
-//   8 = no workgroup barrier
+//   8 = no workgroup barrier, 64 = no row staging, 128 = no LDS transpose
+//   (r01, 8 pairs: full 31.0 ms; 1 -> 19.0, 2 -> 26.7, 4 -> 30.4, 8 -> 28.6,
+//    15 -> 16.4, 15|64 -> 15.4, 15|128 -> 13.0, 15|64|128 -> 11.7)
 #ifndef CSE_ABLATE
 #define CSE_ABLATE 0
 #endif
@@ -506,8 +508,10 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                                           (OUT && gout) ? gout + t * B + i : nullptr, i);
             }
             CSE_MARK("rows");
-            store_rows(t + 1);  // other buffer: its last readers passed this frame's barrier
-            load_rows(t + 2);
+            if (!(CSE_ABLATE & 64)) {
+                store_rows(t + 1);  // other buffer: its last readers passed this frame's barrier
+                load_rows(t + 2);
+            }
             wave_sync();  // my wave's S rows complete (cells never span waves)
 
             CSE_MARK("pass1");
@@ -554,7 +558,8 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             {
                 cf* tw_ = (cf*)(smem + opaque(creg + 8 * i));   // V[b][i] at b*TR + i
 #pragma unroll
-                for (int b = 0; b < 16; ++b) tw_[b * TR] = z[b];
+                for (int b = 0; b < 16; ++b)
+                    if (!(CSE_ABLATE & 128)) tw_[b * TR] = z[b];
             }
             wave_sync();  // transpose block written
 
@@ -563,7 +568,10 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             cf v[16];
             {
                 const cf* tr = (const cf*)(smem + opaque(creg + 8 * TR * b2));   // row V[b2][.]
-                if (L == 16) {
+                if (CSE_ABLATE & 128) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) v[r] = z[r];
+                } else if (L == 16) {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) v[r] = tr[r];
                 } else {  // DFT32 = butterfly (lo +- hi) * W32^{r h}, then DFT16
