@@ -16,13 +16,14 @@ CSE_OK = 0
 ALGO = {"NONE": -1, "SS": 0, "WIENER": 1, "MMSE": 2, "OMLSA": 3}
 NOISE = {"percentile": 0, "min_tracking": 1, "true_noise": 2}
 
-# numpy mirror of cse_cell_t (include/cse.h) — 88 bytes
+# numpy mirror of cse_cell_t (include/cse.h) — 96 bytes
 CELL_DTYPE = np.dtype([
     ("algo", np.int32), ("hop", np.int32), ("y_offset", np.int64),
     ("noise_offset", np.int64), ("noise_stride", np.int64), ("clean_offset", np.int64),
-    ("out_offset", np.int64), ("gain_offset", np.int64), ("param", np.float32, (8,)),
+    ("out_offset", np.int64), ("gain_offset", np.int64), ("lag", np.int32),
+    ("reserved", np.int32), ("param", np.float32, (8,)),
 ], align=True)
-assert CELL_DTYPE.itemsize == 88
+assert CELL_DTYPE.itemsize == 96
 
 # numpy mirror of cse_noise_job_t — 40 bytes
 NOISE_JOB_DTYPE = np.dtype([
@@ -83,7 +84,7 @@ def load(path=LIB_PATH):
     lib.cse_istft_norm.restype = i32
     lib.cse_istft_norm.argtypes = [i32, i32, i64, P, P]
     lib.cse_enhance_cells.restype = i32
-    lib.cse_enhance_cells.argtypes = [i32, i64, P, i64, P, P, P, P, P, P, P, P]
+    lib.cse_enhance_cells.argtypes = [i32, i64, P, i64, P, P, P, P, i64, P, P, P, P]
     _lib = lib
     return lib
 

@@ -47,6 +47,7 @@ struct Args {
     const float* noise;
     const double* clean;
     float* y_out;
+    int64_t out_len;
     float* g_out;
     double* sse;
     uint8_t* finite;
@@ -364,6 +365,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     const float2* Ybase = a.Y + wcell[0].y_offset;
     const float* Nbase = a.noise + wcell[0].noise_offset;
     const int nstride = (int)wcell[0].noise_stride;
+    const int lag = wcell[0].lag;  // shared by the slot group (host-validated)
     const double* cbase = (a.clean && wcell[0].clean_offset >= 0) ? a.clean + wcell[0].clean_offset
                                                                   : nullptr;
     const int T = 1 + len / HOP;
@@ -372,12 +374,15 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 
     // ---- my cell
     const bool valid = cslot < n_cells_wg && wcell[cslot].algo == ALGO;
+    // waveform output (any variant) and gain output (OUT variant only)
+    const bool want_y = a.y_out != nullptr;  // uniform
+    const int out_len = (int)a.out_len;
     float* yout = nullptr;
     float* gout = nullptr;
-    if (OUT && valid) {
+    if (valid) {
         const cse_cell_t* cp = wcell + cslot;
-        if (cp->out_offset >= 0 && a.y_out) yout = a.y_out + cp->out_offset;
-        if (cp->gain_offset >= 0 && a.g_out) gout = a.g_out + cp->gain_offset;
+        if (want_y && cp->out_offset >= 0) yout = a.y_out + cp->out_offset;
+        if (OUT && cp->gain_offset >= 0 && a.g_out) gout = a.g_out + cp->gain_offset;
     }
 
     // ---- workgroup tables: pass-1 twiddles e^{2πi i b/M} [b-1][i], lane
@@ -438,7 +443,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 #pragma unroll
         for (int u = 0; u < W::CPT; ++u) {
             const int j = tid + u * W::THREADS;
-            const int o = t * HOP - NFFT / 2 + j;
+            const int o = t * HOP - NFFT / 2 + j + lag;  // clean sample scored against y[o - lag]
             pc[u] = (j < HOP && cbase && o >= 0 && o < len) ? (float)cbase[o] : 0.0f;
         }
     };
@@ -617,8 +622,12 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             const float* crow_t = (const float*)(smem + opaque(W::OFF_C + (t & 1) * W::HMAX * 4 +
                                                                4 * off));
             // frame t retires output positions [t*HOP - NFFT/2, (t+1)*HOP - NFFT/2)
+            // interior: every slot o and its scored clean index o + lag lie in [0, len)
             const bool edge = (t < R - 1) || (t >= nf);
-            const bool interior = !edge && (t + 1) * HOP - NFFT / 2 <= len;  // uniform
+            const int lo = t * HOP - NFFT / 2;
+            const bool interior = !edge && lo + (lag < 0 ? lag : 0) >= 0 &&
+                                  lo + HOP + (lag > 0 ? lag : 0) <= len;  // uniform
+            const bool head = want_y && lo < out_len;                      // uniform
             float inv[F];
             if (R == 2) {
                 const float* it = (const float*)(smem + opaque(W::OFF_IWS + 4 * W::ISTR * i));
@@ -637,7 +646,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     const int n = SP * (q >> 1) + (q & 1);
                     const float y = done[q] * inv[q];
                     chk = fmaf(y, 0.0f, chk);
-                    if (OUT && yout) yout[o0 + n] = y;
+                    if (head && yout && o0 + n < out_len) yout[o0 + n] = y;
                     const float d = crow_t[n] - fminf(fmaxf(y, -1.0f), 1.0f);
                     part = fmaf(d, d, part);
                 }
@@ -662,10 +671,12 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     }
                     if (o >= 0 && o < len) {
                         const float y = done[q] * iv;
-                        chk = fmaf(y, 0.0f, chk);
-                        if (OUT && yout) yout[o] = y;
-                        const float d = crow_t[n] - fminf(fmaxf(y, -1.0f), 1.0f);
-                        part = fmaf(d, d, part);
+                        if (head && yout && o < out_len) yout[o] = y;
+                        if (o + lag >= 0 && o + lag < len) {  // dropped by the alignment otherwise
+                            chk = fmaf(y, 0.0f, chk);
+                            const float d = crow_t[n] - fminf(fmaxf(y, -1.0f), 1.0f);
+                            part = fmaf(d, d, part);
+                        }
                     }
                 }
             }
@@ -701,8 +712,8 @@ __device__ __forceinline__ void dispatch_algo(const Args& a, const cse_cell_t* w
     }
 }
 
-// OUT: the y_out / g_out variant (parity tests, single-cell plugin calls);
-// the grid/bench path computes only the per-cell score sums.
+// OUT: the g_out (gain matrix) variant for parity tests; waveform output
+// (y_out, any out_len) is available in both variants at run time.
 template <int NFFT, bool OUT>
 __global__ void __launch_bounds__(WG<NFFT>::THREADS, CSE_WAVES_PER_SIMD) enhance_kernel(Args a) {
     using W = WG<NFFT>;
@@ -728,8 +739,8 @@ using namespace cse;
 
 extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
                                  const float* Y, const float* noise, const double* clean,
-                                 float* y_out, float* g_out, double* sse, uint8_t* finite,
-                                 cse_stream_t stream) {
+                                 float* y_out, int64_t out_len, float* g_out, double* sse,
+                                 uint8_t* finite, cse_stream_t stream) {
     CSE_CHECK_ARG(n_fft == 512 || n_fft == 1024, "cse_enhance_cells: n_fft=%d (512|1024)", n_fft);
     CSE_CHECK_ARG(cells && Y && noise, "cse_enhance_cells: NULL cells/Y/noise");
     CSE_CHECK_ARG(len >= 1 && len < (1ll << 30) && n_cells >= 0,
@@ -743,13 +754,16 @@ extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells
     a.noise = noise;
     a.clean = clean;
     a.y_out = y_out;
+    a.out_len = y_out ? out_len : 0;
     a.g_out = g_out;
     a.sse = sse;
     a.finite = finite;
     const int per = CSE_CELLS_PER_GROUP(n_fft);
     const int64_t groups = (n_cells + per - 1) / per;
     CSE_CHECK_ARG(groups < (1ll << 31), "cse_enhance_cells: too many cells");
-    const bool out = (y_out != nullptr) || (g_out != nullptr);
+    CSE_CHECK_ARG(!y_out || (out_len >= 0 && out_len <= len),
+                  "cse_enhance_cells: out_len=%lld not in [0, len]", (long long)out_len);
+    const bool out = g_out != nullptr;  // the gain-writing variant
     const void* fn;
     int bytes, threads;
     if (n_fft == 512) {

@@ -327,7 +327,8 @@ class GridPlan:
         _lib.check(self.eng.lib.cse_enhance_cells(
             self.n_fft, self.L, _ptr(self.cells_d), self.n_packed, _ptr(self.Ybuf),
             _ptr(self.pool), _ptr(self.clean),
-            _ptr(self.y_all), _ptr(self.g_out), _ptr(self.sse_d), _ptr(self.fin_d), _stream()),
+            _ptr(self.y_all), self.L if self.y_all is not None else 0, _ptr(self.g_out),
+            _ptr(self.sse_d), _ptr(self.fin_d), _stream()),
             "cse_enhance_cells")
 
     def execute(self, noisy, clean=None):
@@ -399,7 +400,7 @@ class MultiPlan:
 def pack_waves(cells, n_fft):
     """Group cells into workgroup slot groups (CSE_CELLS_PER_GROUP cells each).
 
-    A slot group's cells must share (algo, hop, spectrum, noise, clean) — the
+    A slot group's cells must share (algo, hop, spectrum, noise, clean, lag) — the
     kernel stages those rows once per workgroup.  Returns (packed cells incl.
     CSE_ALGO_NONE padding, order) with order[i] = index into ``cells`` of packed
     slot i, or -1 for padding.  Groups are ordered longest-first (frames x
@@ -411,7 +412,7 @@ def pack_waves(cells, n_fft):
     groups = {}
     for i, c in enumerate(cells):
         key = (int(c["hop"]), int(c["algo"]), int(c["y_offset"]), int(c["noise_offset"]),
-               int(c["noise_stride"]), int(c["clean_offset"]))
+               int(c["noise_stride"]), int(c["clean_offset"]), int(c["lag"]))
         groups.setdefault(key, []).append(i)
     slots = []
     for key, idxs in groups.items():

@@ -63,8 +63,9 @@ enum {
  * Cells are processed CSE_CELLS_PER_GROUP(n_fft) at a time by one 192-thread
  * workgroup (3 wavefronts) that stages their shared rows in LDS, so the cells
  * of one such slot group (cells[g*G .. g*G+G-1]) MUST share algo, hop,
- * y_offset, noise_offset, noise_stride and clean_offset; pad a short group
- * with CSE_ALGO_NONE slots.  Only param, out_offset and gain_offset may differ.
+ * y_offset, noise_offset, noise_stride, clean_offset and lag; pad a short
+ * group with CSE_ALGO_NONE slots.  Only param, out_offset and gain_offset may
+ * differ.
  */
 typedef struct cse_cell {
     int32_t algo;          /* CSE_ALGO_* */
@@ -76,8 +77,13 @@ typedef struct cse_cell {
     int64_t clean_offset;  /* offset (doubles) of the clean reference for the SNR, or -1 */
     int64_t out_offset;    /* offset (floats) of this cell's output waveform in y_out, or -1 */
     int64_t gain_offset;   /* offset (floats) of this cell's gain matrix G[T][B] in g_out, or -1 */
+    int32_t lag;           /* alignment lag l of the SNR sum (finalize_enhanced): output sample
+                              y[o] is scored against clean[o + l]; samples with o + l outside
+                              [0, len) are dropped (speech_enhancement_comparison.py:61-69).
+                              0 = unaligned.  |lag| < len. */
+    int32_t reserved;      /* 0 */
     float param[8];        /* algorithm parameters, order as in the CSE_ALGO_* comments */
-} cse_cell_t;              /* 88 bytes */
+} cse_cell_t;              /* 96 bytes */
 
 #define CSE_CELLS_PER_GROUP(n_fft) ((n_fft) == 512 ? 12 : 6)
 
@@ -187,18 +193,22 @@ int cse_istft_norm(int n_fft, int hop, int64_t len, float* out, cse_stream_t str
  * (decision-directed a-priori SNR, serial over frames), S = Y*G (SS: noisy
  * phase), inverse real FFT, periodic-Hann synthesis window, overlap-add,
  * window-sum-square normalisation (librosa istft, length = len), and the
- * per-cell score reductions:
- *   sse[c]    = sum_n (clean[n] - clip(y[n], -1, 1))^2   (f64; clean is f64 [..][len],
+ * per-cell score reductions, with l = cell.lag:
+ *   sse[c]    = sum over o in [0,len) with o+l in [0,len) of
+ *               (clean[o + l] - clip(y[o], -1, 1))^2   (f64; clean is f64 [..][len],
  *               used if clean_offset >= 0)
- *   finite[c] = 1 if every y[n] is finite
- * Optional outputs: y_out (the enhanced waveform, f32, [len] at out_offset)
- * and g_out (the gain matrix, f32 [T][B] at gain_offset).
+ *   finite[c] = 1 if every scored y[o] is finite
+ * (the samples an aligned output gets as zero padding are not included: see
+ * cse_xcorr_lag's zero_energy).
+ * Optional outputs: y_out (the first out_len samples of the enhanced waveform,
+ * f32, at out_offset; out_len = len for the whole waveform) and g_out (the
+ * gain matrix, f32 [T][B] at gain_offset).
  * n_fft in {512, 1024}; hop in {128, 256}.
  */
 int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
                       const float* Y, const float* noise, const double* clean,
-                      float* y_out, float* g_out, double* sse, uint8_t* finite,
-                      cse_stream_t stream);
+                      float* y_out, int64_t out_len, float* g_out, double* sse,
+                      uint8_t* finite, cse_stream_t stream);
 
 #ifdef __cplusplus
 }

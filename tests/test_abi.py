@@ -34,14 +34,14 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_version_and_error_channel(lib):
-    assert lib.cse_version() == 1
+    assert lib.cse_version() == 2
     rc = lib.cse_stft(None, None, 1, 100, 512, 128, None, None, None)
     assert rc == -1
     assert b"x is NULL" in lib.cse_last_error()
     rc = lib.cse_stft(ctypes.c_void_p(16), None, 1, 100, 500, 128, None, None, None)
     assert rc == -1 and b"n_fft" in lib.cse_last_error()
     rc = lib.cse_enhance_cells(256, 100, ctypes.c_void_p(16), 1, ctypes.c_void_p(16),
-                               ctypes.c_void_p(16), None, None, None, None, None, None)
+                               ctypes.c_void_p(16), None, None, 0, None, None, None, None)
     assert rc == -1 and b"n_fft" in lib.cse_last_error()
     rc = lib.cse_noise_estimate(7, ctypes.c_void_p(16), 1, 100, 257, 20.0, 1e-10,
                                 ctypes.c_void_p(16), ctypes.c_void_p(16), None)
@@ -49,10 +49,11 @@ def test_version_and_error_channel(lib):
 
 
 def test_cell_struct_layout():
-    assert _lib.CELL_DTYPE.itemsize == 88
+    assert _lib.CELL_DTYPE.itemsize == 96
     off = {n: _lib.CELL_DTYPE.fields[n][1] for n in _lib.CELL_DTYPE.names}
     assert off == {"algo": 0, "hop": 4, "y_offset": 8, "noise_offset": 16, "noise_stride": 24,
-                   "clean_offset": 32, "out_offset": 40, "gain_offset": 48, "param": 56}
+                   "clean_offset": 32, "out_offset": 40, "gain_offset": 48, "lag": 56,
+                   "reserved": 60, "param": 64}
 
 
 def test_workspace_size_is_positive(lib):
@@ -72,7 +73,7 @@ def test_wave_packing_groups_and_pads():
     for w in range(len(packed) // G):
         slots = packed[G * w:G * w + G]
         real = slots[slots["algo"] >= 0]
-        for f in ("hop", "algo", "y_offset", "noise_offset", "noise_stride", "clean_offset"):
+        for f in ("hop", "algo", "y_offset", "noise_offset", "noise_stride", "clean_offset", "lag"):
             assert len(set(slots[f].tolist() if f != "algo" else real[f].tolist())) == 1, f
         assert slots[0]["algo"] >= 0
     # longest first: hop 128 OMLSA before hop 128 SS and hop 256 OMLSA
