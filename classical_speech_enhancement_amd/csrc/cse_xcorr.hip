@@ -1,0 +1,423 @@
+// Alignment lag of finalize_enhanced (speech_enhancement_comparison.py:38-69,
+// 92-106): for every cell, the cross-correlation of the mean-removed first
+// n = min(len, 2 s) samples of the clean reference and of the enhanced output,
+//   c(l) = sum_m r0[m + l] s0[m],   |l| <= max_lag (0.1 s),
+// scipy.signal.correlate(r0, s0, 'full') restricted to the kept lags (:50-58),
+// and lag = the first l of maximal c (np.argmax over ascending lags, :60).
+//
+// Blocked FFT correlation.  The output head e[0, n) is cut into blocks of
+// XB = 4096 samples; block b correlates with the clean window
+// r0[bXB - max_lag, bXB + XB + max_lag) (7296 <= XN = 8192 samples, so the
+// circular correlation of length XN has no wrap-around in the kept lags):
+//   C(f) = sum_b R_b(f) conj(S_b(f)),   c_raw = irfft(C) on lags 0..2 max_lag,
+// one inverse transform per cell.  R_b (the clean side) is computed once per
+// signal by xcorr_prep_kernel.  The mean of e enters as
+//   c(l) = c_raw(l) - mean(e) * W(l),  W(l) = sum of r0 over the overlap of l.
+// Real transforms of XN points are complex 4096-point FFTs (radix-16
+// Stockham, three passes through 32 KiB of LDS) with the usual even/odd
+// packing.
+//
+// Exactness: the fp32 FFT value of every lag is within a small multiple of
+// 1e-6 ||r0|| ||s0|| of the exact one, so every lag within
+// delta = 2e-5 ||r0|| ||s0|| of the fp32 maximum is re-evaluated by a direct
+// fp64 sum and the lag is chosen among those (ties -> smallest lag, like
+// np.argmax).  More than XCAND such candidates (a flat correlation) keeps the
+// fp32 argmax and reports status CSE_XCORR_AMBIGUOUS.
+#include "cse_common.hpp"
+
+namespace cse {
+
+constexpr int XN = 8192;      // real transform length of one block correlation
+constexpr int XH = XN / 2;    // complex FFT length
+constexpr int XB = 4096;      // output samples per block
+constexpr int XT = 256;       // threads per workgroup
+constexpr int XCAND = 64;     // candidates re-evaluated in fp64
+
+// forward (DIR = -1) / inverse (DIR = +1, unnormalised) 4096-point FFT in LDS,
+// radix-16 Stockham (Govindaraju et al. 2008 form): 3 passes, natural order out
+template <int DIR>
+__device__ void fft4096(cf* buf) {
+    const int j = threadIdx.x;
+#pragma unroll 1
+    for (int ns = 1; ns < XH; ns *= 16) {
+        cf v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = buf[j + r * (XH / 16)];
+        const int k = j % ns;
+        if (ns > 1) {
+#pragma unroll
+            for (int r = 1; r < 16; ++r) {
+                float s, c;
+                sincospif((float)(DIR * 2 * r * k) / (float)(ns * 16), &s, &c);
+                v[r] = cmul(v[r], cmk(c, s));
+            }
+        }
+        if (DIR > 0) {
+            idft16(v);
+        } else {  // forward = conj(inverse(conj(v)))
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r].y = -v[r].y;
+            idft16(v);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r].y = -v[r].y;
+        }
+        __syncthreads();
+        const int base = (j / ns) * ns * 16 + k;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) buf[base + r * ns] = v[r];
+        __syncthreads();
+    }
+}
+
+// X(f), f = 0..XH, of the real sequence x[2m] + i x[2m+1] = buf[m] after fft4096<-1>:
+// X(f) = E + e^{-2πi f/XN} O,  E = (Z_f + conj Z_{XH-f})/2,  O = (Z_f - conj Z_{XH-f})/(2i)
+__device__ __forceinline__ cf rfft_bin(const cf* buf, int f) {
+    if (f == XH) return cmk(buf[0].x - buf[0].y, 0.0f);
+    const cf z = buf[f];
+    const cf w = buf[(XH - f) & (XH - 1)];
+    const cf e = cmk(0.5f * (z.x + w.x), 0.5f * (z.y - w.y));
+    const cf o = cmk(0.5f * (z.y + w.y), -0.5f * (z.x - w.x));
+    float s, c;
+    sincospif(-(float)(2 * f) / (float)XN, &s, &c);
+    return cadd(e, cmul(cmk(c, s), o));
+}
+
+// ---------------------------------------------------------------------------
+// per signal: R_b for every block (blockIdx.x < nb), and (blockIdx.x == nb)
+// r0 in fp64, W(l), the zero-padding energies Z(l) and ||r0||^2
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(XT) xcorr_prep_kernel(const double* __restrict__ clean,
+                                                         int64_t len, int n, int max_lag, int nb,
+                                                         float2* __restrict__ R,
+                                                         double* __restrict__ r0buf,
+                                                         double* __restrict__ W,
+                                                         double* __restrict__ Z,
+                                                         double* __restrict__ rnorm) {
+    __shared__ cf buf[XH];
+    __shared__ double red[XT];
+    const int sig = blockIdx.y, tid = threadIdx.x;
+    const double* c = clean + (int64_t)sig * len;
+    // mean of clean[0, n)
+    double acc = 0.0;
+    for (int q = tid; q < n; q += XT) acc += c[q];
+    red[tid] = acc;
+    __syncthreads();
+    for (int s = XT / 2; s > 0; s >>= 1) {
+        if (tid < s) red[tid] += red[tid + s];
+        __syncthreads();
+    }
+    const double mu = red[0] / n;
+    __syncthreads();
+    const int b = blockIdx.x;
+    if (b < nb) {
+        // window r0[b XB - max_lag + v], v < XB + 2 max_lag, zero elsewhere
+        for (int m = tid; m < XH; m += XT) {
+            float xv[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int v = 2 * m + e;
+                const int q = b * XB - max_lag + v;
+                xv[e] = (v < XB + 2 * max_lag && q >= 0 && q < n) ? (float)(c[q] - mu) : 0.0f;
+            }
+            buf[m] = cmk(xv[0], xv[1]);
+        }
+        __syncthreads();
+        fft4096<-1>(buf);
+        float2* out = R + ((int64_t)sig * nb + b) * (XH + 1);
+        for (int f = tid; f <= XH; f += XT) {
+            const cf x = rfft_bin(buf, f);
+            out[f] = make_float2(x.x, x.y);
+        }
+        return;
+    }
+    // block nb: fp64 tables (serial prefix sums are short: <= max_lag terms each side)
+    double* r0 = r0buf + (int64_t)sig * n;
+    double sq = 0.0;
+    for (int q = tid; q < n; q += XT) {
+        const double v = c[q] - mu;
+        r0[q] = v;
+        sq += v * v;
+    }
+    red[tid] = sq;
+    __syncthreads();
+    for (int s = XT / 2; s > 0; s >>= 1) {
+        if (tid < s) red[tid] += red[tid + s];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        rnorm[sig] = red[0];
+        double total = 0.0;
+        for (int q = 0; q < n; ++q) total += r0[q];
+        double* w = W + (int64_t)sig * (2 * max_lag + 1) + max_lag;
+        double* z = Z + (int64_t)sig * (2 * max_lag + 1) + max_lag;
+        w[0] = total;
+        z[0] = 0.0;
+        double head = 0.0, tail = 0.0, zh = 0.0, zt = 0.0;
+        for (int l = 1; l <= max_lag; ++l) {
+            head += r0[l - 1];  // sum_{q < l} r0[q]
+            tail += r0[n - l];  // sum_{q >= n - l} r0[q]
+            w[l] = total - head;
+            w[-l] = total - tail;
+            zh += c[l - 1] * c[l - 1];              // clean energy of the l padded head samples
+            zt += c[len - l] * c[len - l];          // ... of the l padded tail samples
+            z[l] = zh;
+            z[-l] = zt;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// per cell: the lag (see the file comment)
+// ---------------------------------------------------------------------------
+struct XcArgs {
+    const float* head;      // output heads, cell c's at head + head_offset[c]
+    const int64_t* head_offset;
+    const int* sig_of;      // [n_cells]
+    const float2* R;
+    const double* r0buf;
+    const double* W;
+    const double* Z;
+    const double* rnorm;
+    int n, max_lag, nb;
+    int* lag;
+    double* zero_energy;
+    int* status;
+    float* corr;            // optional [n_cells][2 max_lag + 1]
+};
+
+__device__ __forceinline__ double block_sum(double v, double* red) {
+    const int tid = threadIdx.x;
+    __syncthreads();
+    red[tid] = v;
+    __syncthreads();
+    for (int s = XT / 2; s > 0; s >>= 1) {
+        if (tid < s) red[tid] += red[tid + s];
+        __syncthreads();
+    }
+    return red[0];
+}
+
+__global__ void __launch_bounds__(XT) xcorr_lag_kernel(XcArgs a) {
+    __shared__ cf buf[XH];
+    __shared__ double red[XT];
+    __shared__ float rv[XT];
+    __shared__ int ri[XT];
+    __shared__ int cand[XCAND];
+    __shared__ int ncand;
+    const int cell = blockIdx.x, tid = threadIdx.x;
+    const int sig = a.sig_of[cell];
+    const float* e = a.head + a.head_offset[cell];
+    const int n = a.n, L = a.max_lag;
+
+    // mean and energy of e[0, n)
+    double s1 = 0.0, s2 = 0.0;
+    for (int m = tid; m < n; m += XT) {
+        const double v = e[m];
+        s1 += v;
+        s2 += v * v;
+    }
+    s1 = block_sum(s1, red);
+    s2 = block_sum(s2, red);
+    if (!__builtin_isfinite(s1) || !__builtin_isfinite(s2)) {
+        if (tid == 0) {
+            a.lag[cell] = 0;
+            a.zero_energy[cell] = 0.0;
+            a.status[cell] = CSE_XCORR_NONFINITE;
+        }
+        return;
+    }
+    const double mu = s1 / n;
+    const double snorm = fmax(s2 - n * mu * mu, 0.0);
+
+    // C(f) = sum_b R_b(f) conj(S_b(f)); thread owns f = tid + XT r (+ f = XH on thread 0)
+    cf C[16];
+    cf Cn = cmk(0.0f, 0.0f);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) C[r] = cmk(0.0f, 0.0f);
+    const float2* Rs = a.R + (int64_t)sig * a.nb * (XH + 1);
+#pragma unroll 1
+    for (int b = 0; b < a.nb; ++b) {
+        for (int m = tid; m < XH; m += XT) {
+            const int q0 = b * XB + 2 * m;
+            const float x0 = (2 * m < XB && q0 < n) ? e[q0] : 0.0f;
+            const float x1 = (2 * m + 1 < XB && q0 + 1 < n) ? e[q0 + 1] : 0.0f;
+            buf[m] = cmk(x0, x1);
+        }
+        __syncthreads();
+        fft4096<-1>(buf);
+        const float2* Rb = Rs + (int64_t)b * (XH + 1);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = tid + XT * r;
+            const cf s = rfft_bin(buf, f);
+            const float2 rr = Rb[f];
+            // R conj(S)
+            C[r].x += rr.x * s.x + rr.y * s.y;
+            C[r].y += rr.y * s.x - rr.x * s.y;
+        }
+        if (tid == 0) {
+            const cf s = rfft_bin(buf, XH);
+            const float2 rr = Rb[XH];
+            Cn.x += rr.x * s.x + rr.y * s.y;
+            Cn.y += rr.y * s.x - rr.x * s.y;
+        }
+        __syncthreads();
+    }
+    // inverse real transform: Zi(f) = (C_f + conj C_{XH-f}) + i e^{+2πi f/XN} (C_f - conj C_{XH-f})
+#pragma unroll
+    for (int r = 0; r < 16; ++r) buf[tid + XT * r] = C[r];
+    __shared__ cf cnyq;
+    if (tid == 0) cnyq = Cn;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int f = tid + XT * r;
+        const cf cf_ = C[r];
+        const cf cm = (f == 0) ? cnyq : buf[XH - f];
+        const cf ev = cmk(cf_.x + cm.x, cf_.y - cm.y);
+        const cf od = cmk(cf_.x - cm.x, cf_.y + cm.y);
+        float s, c;
+        sincospif((float)(2 * f) / (float)XN, &s, &c);
+        const cf t = cmul(cmk(c, s), od);
+        C[r] = cmk(ev.x - t.y, ev.y + t.x);  // ev + i t
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) buf[tid + XT * r] = C[r];
+    __syncthreads();
+    fft4096<1>(buf);
+
+    // c(l) = c_raw(l) - mu W(l); c_raw[k] = (k even ? Re : Im) buf[k/2] / XN, k = l + L
+    const double* Ws = a.W + (int64_t)sig * (2 * L + 1);
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int k = tid; k <= 2 * L; k += XT) {
+        const cf z = buf[k >> 1];
+        const float craw = ((k & 1) ? z.y : z.x) * (1.0f / XN);
+        const float v = craw - (float)(mu * Ws[k]);
+        if (a.corr) a.corr[(int64_t)cell * (2 * L + 1) + k] = v;
+        if (v > best) {  // k ascending per thread: first max kept
+            best = v;
+            bi = k;
+        }
+    }
+    rv[tid] = best;
+    ri[tid] = bi;
+    __syncthreads();
+    for (int s = XT / 2; s > 0; s >>= 1) {
+        if (tid < s) {
+            const float v2 = rv[tid + s];
+            const int i2 = ri[tid + s];
+            if (v2 > rv[tid] || (v2 == rv[tid] && i2 < ri[tid])) {
+                rv[tid] = v2;
+                ri[tid] = i2;
+            }
+        }
+        __syncthreads();
+    }
+    const float cmax = rv[0];
+    const int kmax = ri[0];
+    const float delta = (float)(2e-5 * sqrt(a.rnorm[sig] * snorm)) + 1e-30f;
+    if (tid == 0) ncand = 0;
+    __syncthreads();
+    for (int k = tid; k <= 2 * L; k += XT) {
+        const cf z = buf[k >> 1];
+        const float v = ((k & 1) ? z.y : z.x) * (1.0f / XN) - (float)(mu * Ws[k]);
+        if (v >= cmax - delta) {
+            const int slot = atomicAdd(&ncand, 1);
+            if (slot < XCAND) cand[slot] = k;
+        }
+    }
+    __syncthreads();
+    const int nc = ncand;
+    int kbest = kmax;
+    int status = CSE_XCORR_OK;
+    if (nc > XCAND) {
+        status = CSE_XCORR_AMBIGUOUS;
+    } else if (nc > 1) {
+        // exact fp64 re-evaluation: c(l) = sum over the overlap of r0[m + l] (e[m] - mu)
+        const double* r0 = a.r0buf + (int64_t)sig * n;
+        double bestd = -INFINITY;
+        kbest = 0x7fffffff;
+        for (int ci = 0; ci < nc; ++ci) {
+            const int k = cand[ci];
+            const int l = k - L;
+            const int m0 = l < 0 ? -l : 0, m1 = l > 0 ? n - l : n;
+            double acc = 0.0;
+            for (int m = m0 + tid; m < m1; m += XT) acc += r0[m + l] * ((double)e[m] - mu);
+            acc = block_sum(acc, red);
+            if (acc > bestd || (acc == bestd && k < kbest)) {
+                bestd = acc;
+                kbest = k;
+            }
+        }
+    }
+    if (tid == 0) {
+        const int l = kbest - L;
+        a.lag[cell] = l;
+        a.zero_energy[cell] = a.Z[(int64_t)sig * (2 * L + 1) + kbest];
+        a.status[cell] = status;
+    }
+}
+
+}  // namespace cse
+
+using namespace cse;
+
+extern "C" int64_t cse_xcorr_workspace_bytes(int64_t n_sig, int64_t len, int n, int max_lag) {
+    if (n_sig < 0 || n < 1 || max_lag < 0) return -1;
+    const int nb = (n + XB - 1) / XB;
+    const int64_t w = 2 * (int64_t)max_lag + 1;
+    return n_sig * nb * (XH + 1) * 8 + n_sig * (int64_t)n * 8 + 2 * n_sig * w * 8 + n_sig * 8 + 256;
+}
+
+extern "C" int cse_xcorr_prepare(const double* clean, int64_t n_sig, int64_t len, int n,
+                                 int max_lag, void* workspace, cse_stream_t stream) {
+    CSE_CHECK_ARG(clean && workspace, "cse_xcorr_prepare: NULL clean/workspace");
+    CSE_CHECK_ARG(n >= 1 && n <= len && max_lag >= 0 && max_lag < n && max_lag <= (XN - XB) / 2,
+                  "cse_xcorr_prepare: n=%d len=%lld max_lag=%d", n, (long long)len, max_lag);
+    const int nb = (n + XB - 1) / XB;
+    unsigned char* ws = (unsigned char*)workspace;
+    float2* R = (float2*)ws;
+    double* r0 = (double*)(ws + n_sig * nb * (XH + 1) * 8);
+    double* W = r0 + n_sig * (int64_t)n;
+    double* Z = W + n_sig * (2 * (int64_t)max_lag + 1);
+    double* rn = Z + n_sig * (2 * (int64_t)max_lag + 1);
+    hipLaunchKernelGGL(xcorr_prep_kernel, dim3(nb + 1, (unsigned)n_sig), dim3(XT), 0,
+                       (hipStream_t)stream, clean, len, n, max_lag, nb, R, r0, W, Z, rn);
+    CSE_CHECK_LAUNCH("cse_xcorr_prepare");
+    return CSE_OK;
+}
+
+extern "C" int cse_xcorr_lag(const float* head, const int64_t* head_offset, const int32_t* sig_of,
+                             int64_t n_cells, int64_t n_sig, int n, int max_lag,
+                             const void* workspace, int32_t* lag, double* zero_energy,
+                             int32_t* status, float* corr, cse_stream_t stream) {
+    CSE_CHECK_ARG(head && head_offset && sig_of && workspace && lag && zero_energy && status,
+                  "cse_xcorr_lag: NULL argument");
+    CSE_CHECK_ARG(n >= 1 && max_lag >= 0 && max_lag < n && max_lag <= (XN - XB) / 2,
+                  "cse_xcorr_lag: n=%d max_lag=%d", n, max_lag);
+    if (n_cells == 0) return CSE_OK;
+    const int nb = (n + XB - 1) / XB;
+    const unsigned char* ws = (const unsigned char*)workspace;
+    XcArgs a;
+    a.head = head;
+    a.head_offset = head_offset;
+    a.sig_of = sig_of;
+    a.R = (const float2*)ws;
+    a.r0buf = (const double*)(ws + n_sig * nb * (XH + 1) * 8);
+    a.W = a.r0buf + n_sig * (int64_t)n;
+    a.Z = a.W + n_sig * (2 * (int64_t)max_lag + 1);
+    a.rnorm = a.Z + n_sig * (2 * (int64_t)max_lag + 1);
+    a.n = n;
+    a.max_lag = max_lag;
+    a.nb = nb;
+    a.lag = lag;
+    a.zero_energy = zero_energy;
+    a.status = status;
+    a.corr = corr;
+    hipLaunchKernelGGL(xcorr_lag_kernel, dim3((unsigned)n_cells), dim3(XT), 0,
+                       (hipStream_t)stream, a);
+    CSE_CHECK_LAUNCH("cse_xcorr_lag");
+    return CSE_OK;
+}

@@ -31,6 +31,12 @@ ALGOS = {
 ALIASES = {"ss": "spectralSubtractor", "spectral_subtraction": "spectralSubtractor",
            "wiener_filter": "wiener", "advanced_mmse": "omlsa"}
 DEFAULTS = {"mmse": {"noise_mu": 0.98, "gain_max": 1.0}, "omlsa": {"v_max": 80.0}}
+# finalize_enhanced alignment (speech_enhancement_comparison.py:38-69) at 16 kHz:
+# correlate the first corr_seconds = 2 s, lags within max_shift_s = 0.1 s,
+# no alignment below 256 samples
+ALIGN_CORR_SAMPLES = 32000
+ALIGN_MAX_LAG = 1600
+ALIGN_MIN_SAMPLES = 256
 # relative per-bin cost used to order waves (longest first)
 ALGO_COST = {"SS": 1.0, "WIENER": 1.1, "MMSE": 2.0, "OMLSA": 3.0}
 
@@ -153,11 +159,12 @@ class Engine:
 
     # ------------------------------------------------------------------ grid
     def plan(self, n_signals, length, specs, with_clean=True, want_waveforms=False,
-             want_gains=False):
+             want_gains=False, align=False):
         """Build one GridPlan per n_fft for these specs (see GridPlan)."""
-        return MultiPlan(self, n_signals, length, specs, with_clean, want_waveforms, want_gains)
+        return MultiPlan(self, n_signals, length, specs, with_clean, want_waveforms, want_gains,
+                         align)
 
-    def run(self, noisy, specs, clean=None, want_waveforms=False, want_gains=False):
+    def run(self, noisy, specs, clean=None, want_waveforms=False, want_gains=False, align=False):
         """Enhance every cell spec; returns a dict of per-spec results.
 
         noisy/clean: [S, L] float64 cuda tensors (clean may be None if no spec
@@ -167,7 +174,7 @@ class Engine:
           'y' [n, L] f32 cuda and 'G' list of [T, B] f32 cuda.
         """
         S, L = noisy.shape
-        mp = self.plan(S, L, specs, clean is not None, want_waveforms, want_gains)
+        mp = self.plan(S, L, specs, clean is not None, want_waveforms, want_gains, align)
         mp.execute(noisy, clean)
         return mp.results()
 
@@ -185,7 +192,8 @@ class GridPlan:
     sync, no allocation), so it can be timed or captured as a graph.
     """
 
-    def __init__(self, eng, n_fft, S, L, items, with_clean, want_y, want_g, y_all=None):
+    def __init__(self, eng, n_fft, S, L, items, with_clean, want_y, want_g, y_all=None,
+                 align=False):
         self.eng, self.n_fft, self.S, self.L = eng, n_fft, S, L
         self.items = items
         dev = eng.device
@@ -274,6 +282,29 @@ class GridPlan:
         self.with_clean = with_clean
         # frame-gain evaluations (SURVEY §8(d) unit): sum over cells of frames
         self.units = int(sum(n_frames(L, p["hop_length"]) for (_, _, _, p) in items))
+        # ---- finalize_enhanced alignment (speech_enhancement_comparison.py:38-69)
+        self.rerun = None
+        self.xc_n = min(L, ALIGN_CORR_SAMPLES)
+        self.align = bool(align) and with_clean and self.xc_n >= ALIGN_MIN_SAMPLES
+        if self.align:
+            self.xc_lag_max = min(ALIGN_MAX_LAG, self.xc_n - 1)
+            if y_all is not None:   # whole waveforms requested: their heads are the input
+                self.head = y_all
+                head_off = self.cells["out_offset"].astype(np.int64)
+            else:
+                self.head = torch.empty(len(items) * self.xc_n, dtype=torch.float32, device=dev)
+                head_off = np.arange(len(items), dtype=np.int64) * self.xc_n
+                self.cells["out_offset"] = head_off
+                packed, _ = pack_waves(self.cells, n_fft)
+                self.cells_d = torch.from_numpy(packed.view(np.uint8).copy()).to(dev)
+            self.head_off = torch.as_tensor(head_off, device=dev)
+            self.sig_of = torch.as_tensor(np.array([sig for (_, sig, _, _) in items],
+                                                   dtype=np.int32), device=dev)
+            self.xc_ws = torch.empty(int(eng.lib.cse_xcorr_workspace_bytes(
+                S, L, self.xc_n, self.xc_lag_max)), dtype=torch.uint8, device=dev)
+            self.lag_d = torch.zeros(len(items), dtype=torch.int32, device=dev)
+            self.zero_d = torch.zeros(len(items), dtype=torch.float64, device=dev)
+            self.xst_d = torch.zeros(len(items), dtype=torch.int32, device=dev)
 
     def prepare(self, noisy, clean=None):
         """Group-level analysis: STFTs and every noise row (once per signal batch)."""
@@ -324,16 +355,55 @@ class GridPlan:
 
     def enhance(self):
         """THE HOT PATH launch: every cell of this n_fft, one kernel."""
+        if self.y_all is not None:
+            yo, olen = self.y_all, self.L
+        elif self.align:
+            yo, olen = self.head, self.xc_n
+        else:
+            yo, olen = None, 0
         _lib.check(self.eng.lib.cse_enhance_cells(
             self.n_fft, self.L, _ptr(self.cells_d), self.n_packed, _ptr(self.Ybuf),
-            _ptr(self.pool), _ptr(self.clean),
-            _ptr(self.y_all), self.L if self.y_all is not None else 0, _ptr(self.g_out),
+            _ptr(self.pool), _ptr(self.clean), _ptr(yo), olen, _ptr(self.g_out),
             _ptr(self.sse_d), _ptr(self.fin_d), _stream()),
             "cse_enhance_cells")
 
     def execute(self, noisy, clean=None):
         self.prepare(noisy, clean)
         self.enhance()
+        if self.align:
+            self.finalize()
+
+    def finalize(self):
+        """finalize_enhanced on the device: per-cell cross-correlation lag
+        (cse_xcorr_lag), then the cells whose lag is not 0 are scored again
+        with the shifted output (cse_enhance_cells with cell.lag, plus the
+        clean energy of the zero padding)."""
+        lib, st = self.eng.lib, _stream()
+        _lib.check(lib.cse_xcorr_prepare(_ptr(self.clean), self.S, self.L, self.xc_n,
+                                         self.xc_lag_max, _ptr(self.xc_ws), st),
+                   "cse_xcorr_prepare")
+        _lib.check(lib.cse_xcorr_lag(_ptr(self.head), _ptr(self.head_off), _ptr(self.sig_of),
+                                     len(self.items), self.S, self.xc_n, self.xc_lag_max,
+                                     _ptr(self.xc_ws), _ptr(self.lag_d), _ptr(self.zero_d),
+                                     _ptr(self.xst_d), None, st), "cse_xcorr_lag")
+        lag = self.lag_d.cpu().numpy()
+        sel = np.nonzero(lag != 0)[0]
+        self.rerun = None
+        if len(sel) == 0:
+            return
+        cells = self.cells[sel].copy()
+        cells["lag"] = lag[sel]
+        cells["out_offset"] = -1
+        cells["gain_offset"] = -1
+        packed, order = pack_waves(cells, self.n_fft)
+        cd = torch.from_numpy(packed.view(np.uint8).copy()).to(self.eng.device)
+        sse = torch.zeros(len(packed), dtype=torch.float64, device=self.eng.device)
+        fin = torch.zeros(len(packed), dtype=torch.uint8, device=self.eng.device)
+        _lib.check(lib.cse_enhance_cells(
+            self.n_fft, self.L, _ptr(cd), len(packed), _ptr(self.Ybuf), _ptr(self.pool),
+            _ptr(self.clean), None, 0, None, _ptr(sse), _ptr(fin), st),
+            "cse_enhance_cells(aligned)")
+        self.rerun = (sel, order, sse, fin)
 
     def results(self):
         sse_p = self.sse_d.cpu().numpy()
@@ -343,6 +413,17 @@ class GridPlan:
         fin = np.empty(len(self.items), dtype=bool)
         sse[self.order[real]] = sse_p[real]
         fin[self.order[real]] = fin_p[real]
+        self.lag = self.xstatus = None
+        if self.align:
+            self.lag = self.lag_d.cpu().numpy()
+            self.xstatus = self.xst_d.cpu().numpy()
+            fin &= self.xstatus != _lib.XCORR_NONFINITE
+            if self.rerun is not None:
+                sel, order, sse_r, fin_r = self.rerun
+                sr, fr = sse_r.cpu().numpy(), fin_r.cpu().numpy().astype(bool)
+                ok = order >= 0
+                sse[sel[order[ok]]] = sr[ok] + self.zero_d.cpu().numpy()[sel[order[ok]]]
+                fin[sel[order[ok]]] = fr[ok]
         G = None
         if self.g_out is not None:
             G = [self.g_out[g0:g0 + T * self.B].view(T, self.B) for (g0, T) in self.g_offsets]
@@ -352,8 +433,9 @@ class GridPlan:
 class MultiPlan:
     """GridPlans for every n_fft present in a spec list (spec order preserved)."""
 
-    def __init__(self, eng, S, L, specs, with_clean, want_y, want_g):
+    def __init__(self, eng, S, L, specs, with_clean, want_y, want_g, align=False):
         self.n = len(specs)
+        self.align = align
         self.want_g = want_g
         self.y_all = (torch.zeros((self.n, L), dtype=torch.float32, device=eng.device)
                       if want_y else None)
@@ -371,7 +453,8 @@ class MultiPlan:
                     and n_frames(L, p["hop_length"]) >= 5):
                 raise ValueError("TrueNoiseEstimator requires clean_audio and noisy_audio")
             by_fft.setdefault(int(p["n_fft"]), []).append((idx, int(sig), alg, p))
-        self.plans = [GridPlan(eng, n_fft, S, L, items, with_clean, want_y, want_g, self.y_all)
+        self.plans = [GridPlan(eng, n_fft, S, L, items, with_clean, want_y, want_g, self.y_all,
+                               align)
                       for n_fft, items in sorted(by_fft.items())]
         self.units = sum(p.units for p in self.plans)
 
@@ -383,13 +466,19 @@ class MultiPlan:
         sse = np.full(self.n, np.nan)
         fin = np.zeros(self.n, dtype=bool)
         gains = [None] * self.n if self.want_g else None
+        lag = np.zeros(self.n, dtype=np.int64) if self.align else None
+        xst = np.zeros(self.n, dtype=np.int64) if self.align else None
         for p in self.plans:
             s, f, G = p.results()
             for c, (idx, *_rest) in enumerate(p.items):
                 sse[idx], fin[idx] = s[c], f[c]
                 if gains is not None:
                     gains[idx] = G[c]
+                if lag is not None and p.lag is not None:
+                    lag[idx], xst[idx] = p.lag[c], p.xstatus[c]
         out = {"sse": sse, "finite": fin}
+        if lag is not None:
+            out["lag"], out["xcorr_status"] = lag, xst
         if self.y_all is not None:
             out["y"] = self.y_all
         if gains is not None:

@@ -210,6 +210,44 @@ int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n
                       float* y_out, int64_t out_len, float* g_out, double* sse,
                       uint8_t* finite, cse_stream_t stream);
 
+/*
+ * Alignment of finalize_enhanced (speech_enhancement_comparison.py:38-69, 92-106):
+ * the lag l in [-max_lag, max_lag] maximising the cross-correlation
+ *   c(l) = sum_m r0[m + l] s0[m]   (scipy.signal.correlate(r0, s0, 'full'), :50-58)
+ * of the mean-removed first n samples of the clean reference (r0) and of the
+ * enhanced output (s0); the first maximum in ascending lag order (np.argmax,
+ * :60).  The reference uses n = min(len, 2 s * sr) and max_lag = 0.1 s * sr and
+ * skips alignment when n < 256 (:44-46) — the caller applies those rules.
+ * Requires max_lag <= 2048.
+ *
+ * cse_xcorr_prepare: per-signal tables (FFT blocks of the clean reference,
+ *   fp64 r0, overlap sums, zero-padding energies) into the workspace of
+ *   cse_xcorr_workspace_bytes(n_sig, len, n, max_lag) bytes.  clean: [n_sig][len] f64.
+ * cse_xcorr_lag: per cell c, the cell's output samples y[0, n) at
+ *   head + head_offset[c] (f32, e.g. written by cse_enhance_cells with
+ *   out_len >= n), sig_of[c] = its signal.  Outputs:
+ *     lag[c]          the alignment lag (0 when status is NONFINITE)
+ *     zero_energy[c]  sum of clean^2 over the samples the shifted output leaves
+ *                     as zero padding (l > 0: clean[0, l); l < 0: clean[len+l, len)),
+ *                     to be added to the lag-l sse of cse_enhance_cells
+ *     status[c]       CSE_XCORR_*
+ *     corr            optional [n_cells][2 max_lag + 1] f32 c(l) (diagnostics), or NULL
+ * Lags whose fp32 FFT correlation lies within 2e-5 ||r0|| ||s0|| of the maximum
+ * are re-evaluated exactly in fp64 (at most 64; more -> AMBIGUOUS, fp32 argmax).
+ */
+enum {
+    CSE_XCORR_OK = 0,
+    CSE_XCORR_AMBIGUOUS = 1, /* > 64 near-maximal lags: fp32 argmax kept */
+    CSE_XCORR_NONFINITE = 2, /* non-finite output head: no alignment */
+};
+int64_t cse_xcorr_workspace_bytes(int64_t n_sig, int64_t len, int n, int max_lag);
+int cse_xcorr_prepare(const double* clean, int64_t n_sig, int64_t len, int n, int max_lag,
+                      void* workspace, cse_stream_t stream);
+int cse_xcorr_lag(const float* head, const int64_t* head_offset, const int32_t* sig_of,
+                  int64_t n_cells, int64_t n_sig, int n, int max_lag, const void* workspace,
+                  int32_t* lag, double* zero_energy, int32_t* status, float* corr,
+                  cse_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

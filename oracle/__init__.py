@@ -23,11 +23,11 @@ from .noise_ref import (noise_estimation, percentile_noise, min_tracking_noise,
 from .gain_ref import (spectral_subtraction, wiener_filter, mmse, advanced_mmse,
                        ALGORITHMS)
 from .pipeline_ref import (GRIDS, grid_cells, finalize_enhanced, calculate_snr,
-                           align_to_reference, match_length, to_mono,
+                           align_to_reference, align_lag, match_length, to_mono,
                            combined_score, tolerance_scan)
 
 __all__ = [
-    "stft", "istft", "fix_length", "hann_periodic", "n_frames_for",
+    "stft", "istft", "fix_length", "hann_periodic", "n_frames_for", "align_lag",
     "noise_estimation", "percentile_noise", "min_tracking_noise", "true_noise",
     "simple_noise", "spectral_subtraction", "wiener_filter", "mmse",
     "advanced_mmse", "ALGORITHMS", "GRIDS", "grid_cells", "finalize_enhanced",

@@ -189,6 +189,57 @@ def test_grid_snr_table_matches_reference(P):
                                    err_msg=name)
 
 
+def test_grid_snr_aligned_matches_reference(P):
+    """finalize_enhanced on the device: the reference's own per-cell SNR after
+    cross-correlation alignment (speech_enhancement_comparison.py:92-106), full
+    HEAD grid on a 0.5-s pair — 852 of the 1920 MMSE cells have a non-zero lag."""
+    import torch
+    from classical_speech_enhancement_amd.engine import Engine, snr_db
+    g = load_golden("grid_snr_0p5s.npz")
+    clean, noisy = g["clean"], g["noisy"]
+    eng = Engine()
+    x = torch.as_tensor(noisy).cuda().view(1, -1)
+    c = torch.as_tensor(clean).cuda().view(1, -1)
+    ps = float(np.sum(clean ** 2))
+    moved = 0
+    for short, name in (("ss", "spectralSubtractor"), ("mmse", "mmse"), ("wiener", "wiener"),
+                        ("omlsa", "omlsa")):
+        cells = oracle.grid_cells(oracle.GRIDS[name])
+        res = eng.run(x, [(0, name, p) for p in cells], clean=c, align=True)
+        assert res["finite"].all()
+        assert (res["xcorr_status"] == 0).all()
+        moved += int(np.sum(res["lag"] != 0))
+        snr = snr_db(res["sse"], ps)
+        np.testing.assert_allclose(snr, g[f"snr|{short}"], rtol=0, atol=2e-4, err_msg=name)
+    assert moved >= 800
+
+
+def test_alignment_lags_10s_vs_oracle(P):
+    """10-s pair: device lags and aligned SNR of sampled MMSE / SS cells against
+    the oracle's align_lag / finalize on its own fp64 outputs (n = 32000
+    correlated samples, 8 FFT blocks)."""
+    import torch
+    from classical_speech_enhancement_amd.engine import Engine, snr_db
+    clean, noisy = make_pair(5, seconds=10.0)
+    eng = Engine()
+    x = torch.as_tensor(noisy).cuda().view(1, -1)
+    c = torch.as_tensor(clean).cuda().view(1, -1)
+    rng = np.random.default_rng(1)
+    cells = []
+    for name in ("mmse", "spectralSubtractor"):
+        grid = [p for p in oracle.grid_cells(oracle.GRIDS[name]) if p["n_fft"] == 512]
+        cells += [(name, grid[i]) for i in rng.choice(len(grid), 6, replace=False)]
+    res = eng.run(x, [(0, a, p) for a, p in cells], clean=c, align=True)
+    ps = float(np.sum(clean ** 2))
+    for j, (name, p) in enumerate(cells):
+        y = oracle.ALGORITHMS[name](noisy, 16000, **p)
+        lag = oracle.align_lag(clean, y, 16000)
+        assert res["lag"][j] == (lag or 0), (name, p, res["lag"][j], lag)
+        e = oracle.finalize_enhanced(y, clean, 16000)
+        ref = oracle.calculate_snr(clean, e)
+        assert abs(snr_db(res["sse"][j:j + 1], ps)[0] - ref) < 2e-4, (name, p)
+
+
 def test_full_size_grid_properties():
     """10-s pair, n_fft=512 half of the full grid: finite, deterministic, duplicate
     cells (min_tracking ignores noise_percentile) bit-identical, sampled cells
