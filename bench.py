@@ -125,6 +125,9 @@ def main():
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--align", action="store_true",
+                    help="also run finalize_enhanced's alignment (xcorr lag + lag-shifted rescoring)"
+                         " inside the step (SURVEY §8(f) row 1; not part of the §8(d) timed region)")
     args = ap.parse_args()
 
     import torch
@@ -148,7 +151,7 @@ def main():
     clean_pow = (clean ** 2).sum(dim=1).cpu().numpy()
     L = noisy.shape[1]
     specs = grid_specs(P, 512)
-    mp = eng.plan(P, L, specs, with_clean=True)
+    mp = eng.plan(P, L, specs, with_clean=True, align=args.align)
     plan = mp.plans[0]
     units = mp.units
 
@@ -159,6 +162,8 @@ def main():
         plan.enhance()
         if ev is not None:
             ev[1].record()
+        if args.align:
+            plan.finalize()
         rec = torch.stack([plan.sse_d, plan.fin_d.double()])
         if world > 1:
             if dist.get_backend() == "gloo":
@@ -227,6 +232,7 @@ def main():
             "pairs_per_gpu": P, "clip_s": args.seconds, "sr": 16000, "n_fft": 512,
             "cells_per_gpu": len(specs), "units_per_step_per_gpu": units,
             "parallelism": f"pairs sharded over {world} rank(s), all_gather of per-cell records",
+            "finalize_alignment": bool(args.align),
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",

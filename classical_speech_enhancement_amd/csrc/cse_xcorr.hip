@@ -32,6 +32,9 @@ constexpr int XH = XN / 2;    // complex FFT length
 constexpr int XB = 4096;      // output samples per block
 constexpr int XT = 256;       // threads per workgroup
 constexpr int XCAND = 64;     // candidates re-evaluated in fp64
+#ifndef CSE_XC_WG_PER_CU
+#define CSE_XC_WG_PER_CU 3    // 168 VGPRs + 72 B spill: 4% faster than 2 (192, no spill); 4 spills 240 B
+#endif
 
 // forward (DIR = -1) / inverse (DIR = +1, unnormalised) 4096-point FFT in LDS,
 // radix-16 Stockham (Govindaraju et al. 2008 form): 3 passes, natural order out
@@ -45,11 +48,16 @@ __device__ void fft4096(cf* buf) {
         for (int r = 0; r < 16; ++r) v[r] = buf[j + r * (XH / 16)];
         const int k = j % ns;
         if (ns > 1) {
+            // w^r, w = e^{DIR 2πi k/(16 ns)}: one accurate sincos, then a product
+            // chain (|error| <= 15 ulp, far inside the candidate margin)
+            float s, c;
+            sincospif((float)(DIR * 2 * k) / (float)(ns * 16), &s, &c);
+            const cf w = cmk(c, s);
+            cf wr = w;
 #pragma unroll
             for (int r = 1; r < 16; ++r) {
-                float s, c;
-                sincospif((float)(DIR * 2 * r * k) / (float)(ns * 16), &s, &c);
-                v[r] = cmul(v[r], cmk(c, s));
+                v[r] = cmul(v[r], wr);
+                wr = cmul(wr, w);
             }
         }
         if (DIR > 0) {
@@ -71,15 +79,21 @@ __device__ void fft4096(cf* buf) {
 
 // X(f), f = 0..XH, of the real sequence x[2m] + i x[2m+1] = buf[m] after fft4096<-1>:
 // X(f) = E + e^{-2πi f/XN} O,  E = (Z_f + conj Z_{XH-f})/2,  O = (Z_f - conj Z_{XH-f})/(2i)
-__device__ __forceinline__ cf rfft_bin(const cf* buf, int f) {
+// tw = e^{-2πi f/XN} is passed in (thread-owned bins f = tid + 256 r share
+// e^{-2πi tid/XN} and differ by the compile-time rotor e^{-2πi r/32})
+__device__ __forceinline__ cf rfft_bin(const cf* buf, int f, cf tw) {
     if (f == XH) return cmk(buf[0].x - buf[0].y, 0.0f);
     const cf z = buf[f];
     const cf w = buf[(XH - f) & (XH - 1)];
     const cf e = cmk(0.5f * (z.x + w.x), 0.5f * (z.y - w.y));
     const cf o = cmk(0.5f * (z.y + w.y), -0.5f * (z.x - w.x));
+    return cadd(e, cmul(tw, o));
+}
+
+__device__ __forceinline__ cf bin_rotor(int f) {
     float s, c;
     sincospif(-(float)(2 * f) / (float)XN, &s, &c);
-    return cadd(e, cmul(cmk(c, s), o));
+    return cmk(c, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -125,7 +139,7 @@ __global__ void __launch_bounds__(XT) xcorr_prep_kernel(const double* __restrict
         fft4096<-1>(buf);
         float2* out = R + ((int64_t)sig * nb + b) * (XH + 1);
         for (int f = tid; f <= XH; f += XT) {
-            const cf x = rfft_bin(buf, f);
+            const cf x = rfft_bin(buf, f, bin_rotor(f));
             out[f] = make_float2(x.x, x.y);
         }
         return;
@@ -144,10 +158,19 @@ __global__ void __launch_bounds__(XT) xcorr_prep_kernel(const double* __restrict
         if (tid < s) red[tid] += red[tid + s];
         __syncthreads();
     }
+    const double r2 = red[0];
+    __syncthreads();
+    double tp = 0.0;
+    for (int q = tid; q < n; q += XT) tp += r0[q];
+    red[tid] = tp;
+    __syncthreads();
+    for (int s = XT / 2; s > 0; s >>= 1) {
+        if (tid < s) red[tid] += red[tid + s];
+        __syncthreads();
+    }
     if (tid == 0) {
-        rnorm[sig] = red[0];
-        double total = 0.0;
-        for (int q = 0; q < n; ++q) total += r0[q];
+        rnorm[sig] = r2;
+        const double total = red[0];
         double* w = W + (int64_t)sig * (2 * max_lag + 1) + max_lag;
         double* z = Z + (int64_t)sig * (2 * max_lag + 1) + max_lag;
         w[0] = total;
@@ -197,7 +220,7 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
     return red[0];
 }
 
-__global__ void __launch_bounds__(XT) xcorr_lag_kernel(XcArgs a) {
+__global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs a) {
     __shared__ cf buf[XH];
     __shared__ double red[XT];
     __shared__ float rv[XT];
@@ -235,6 +258,7 @@ __global__ void __launch_bounds__(XT) xcorr_lag_kernel(XcArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) C[r] = cmk(0.0f, 0.0f);
     const float2* Rs = a.R + (int64_t)sig * a.nb * (XH + 1);
+    const cf rot_tid = bin_rotor(tid);
 #pragma unroll 1
     for (int b = 0; b < a.nb; ++b) {
         for (int m = tid; m < XH; m += XT) {
@@ -249,14 +273,15 @@ __global__ void __launch_bounds__(XT) xcorr_lag_kernel(XcArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = tid + XT * r;
-            const cf s = rfft_bin(buf, f);
+            // e^{-2πi (tid + 256 r)/8192} = rot_tid * e^{-2πi r/32}
+            const cf s = rfft_bin(buf, f, cmul(rot_tid, cmk(Rot32::c[r], -Rot32::s[r])));
             const float2 rr = Rb[f];
             // R conj(S)
             C[r].x += rr.x * s.x + rr.y * s.y;
             C[r].y += rr.y * s.x - rr.x * s.y;
         }
         if (tid == 0) {
-            const cf s = rfft_bin(buf, XH);
+            const cf s = rfft_bin(buf, XH, cmk(1.0f, 0.0f));
             const float2 rr = Rb[XH];
             Cn.x += rr.x * s.x + rr.y * s.y;
             Cn.y += rr.y * s.x - rr.x * s.y;
@@ -276,9 +301,8 @@ __global__ void __launch_bounds__(XT) xcorr_lag_kernel(XcArgs a) {
         const cf cm = (f == 0) ? cnyq : buf[XH - f];
         const cf ev = cmk(cf_.x + cm.x, cf_.y - cm.y);
         const cf od = cmk(cf_.x - cm.x, cf_.y + cm.y);
-        float s, c;
-        sincospif((float)(2 * f) / (float)XN, &s, &c);
-        const cf t = cmul(cmk(c, s), od);
+        const cf tw = cmul(rot_tid, cmk(Rot32::c[r], -Rot32::s[r]));  // e^{-2πi f/XN}
+        const cf t = cmul(cmk(tw.x, -tw.y), od);                       // e^{+2πi f/XN} od
         C[r] = cmk(ev.x - t.y, ev.y + t.x);  // ev + i t
     }
     __syncthreads();

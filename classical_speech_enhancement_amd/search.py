@@ -25,9 +25,10 @@ Scores: the reference scores cells by STOI, PESQ and their balance
 (evaluation_metrics.py:30-36, 104-115); pystoi/pesq are not available in this
 image, so the device path scores by SNR of the clipped output
 (evaluation_metrics.py:39-58), the metric the reference reports next to them.
-The SNR here is taken at lag 0 (the synthetic pairs are aligned); the
-cross-correlation alignment of finalize_enhanced (:38-69) is the next §8(f)
-row and is applied on the host in the oracle only.
+Each cell is scored like finalize_enhanced (:92-106): its output is aligned
+to the clean reference by the cross-correlation lag (on the device,
+cse_xcorr_lag), length-matched, checked for finiteness and clipped, then
+calculate_snr.
 """
 
 import math
@@ -103,8 +104,9 @@ def assign_lpt(specs, lengths, world):
     return rank_of, load
 
 
-def engine_compute(clean, noisy, specs, ids, engine=None):
-    """Device compute of the cells ``ids``: per-cell (sse, snr, finite).
+def engine_compute(clean, noisy, specs, ids, engine=None, align=True):
+    """Device compute of the cells ``ids``: per-cell (sse, snr, finite), scored
+    after finalize_enhanced's alignment (align=False: at lag 0).
 
     clean/noisy: lists of 1-D float arrays (host) indexed by pair.  Pairs are
     batched by length (the engine's signal batches are rectangular)."""
@@ -122,7 +124,7 @@ def engine_compute(clean, noisy, specs, ids, engine=None):
         nz = torch.as_tensor(np.stack([np.asarray(noisy[p], np.float64) for p in pairs])).cuda()
         cl = torch.as_tensor(np.stack([np.asarray(clean[p], np.float64) for p in pairs])).cuda()
         sub = [(slot[specs[ids[j]][0]], specs[ids[j]][1], specs[ids[j]][2]) for j in js]
-        res = eng.run(nz, sub, clean=cl)
+        res = eng.run(nz, sub, clean=cl, align=align)
         cpow = (cl ** 2).sum(dim=1).cpu().numpy()
         snr = snr_db(res["sse"], cpow[[s for (s, _, _) in sub]])
         out[js, 0] = res["sse"]

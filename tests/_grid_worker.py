@@ -27,8 +27,11 @@ def pairs(n=3, seconds=0.3):
     return [c for c, _ in out], [x for _, x in out]
 
 
-def oracle_compute(clean, noisy, specs, ids):
-    """Per-cell (sse, snr, finite) from the CPU oracle at lag 0."""
+def oracle_compute(clean, noisy, specs, ids, align=True):
+    """Per-cell (sse, snr, finite) from the CPU oracle: finalize_enhanced
+    (alignment, length match, finiteness, clip) then calculate_snr, like the
+    reference's grid loop (speech_enhancement_comparison.py:165-180); align=False
+    scores the clipped output at lag 0."""
     import oracle
     out = np.zeros((len(ids), 3))
     for j, cid in enumerate(ids):
@@ -37,10 +40,12 @@ def oracle_compute(clean, noisy, specs, ids):
         if kw["noise_method"] == "true_noise":
             kw["clean_audio"] = clean[pair]
         y = oracle.ALGORITHMS[alg](noisy[pair], 16000, **kw)
-        fin = bool(np.all(np.isfinite(y)))
-        e = np.clip(y, -1.0, 1.0)
         c = np.asarray(clean[pair], np.float64)
-        out[j] = (np.sum((c - e) ** 2), oracle.calculate_snr(c, e), fin)
+        e = oracle.finalize_enhanced(y, c, 16000, do_align=align)
+        if e is None:
+            out[j] = (np.nan, np.nan, 0)
+            continue
+        out[j] = (np.sum((c - e) ** 2), oracle.calculate_snr(c, e), 1)
     return out
 
 
