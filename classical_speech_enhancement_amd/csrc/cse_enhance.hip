@@ -593,7 +593,8 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             CSE_MARK("window");
             // ---------------- synthesis window (/n_fft) --------------------
             {
-                const float* wt = (const float*)(smem + opaque(W::OFF_WIN + 4 * W::WSTR * i));
+                const float* wt = (const float*)__builtin_assume_aligned(
+                    smem + opaque(W::OFF_WIN + 4 * W::WSTR * i), 16);
 #pragma unroll
                 for (int q = 0; q < 32; ++q) x[q] = ((q & 1) ? v[q >> 1].y : v[q >> 1].x) * wt[q];
             }
@@ -619,8 +620,8 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         for (int q = 0; q < PEND; ++q) acc[q] = (q + F < PEND ? acc[q + F] : 0.0f) + x[q + F];
         if (valid && !(CSE_ABLATE & 4)) {
             const int o0 = t * HOP + off - NFFT / 2;  // output index of q = 0
-            const float* crow_t = (const float*)(smem + opaque(W::OFF_C + (t & 1) * W::HMAX * 4 +
-                                                               4 * off));
+            const float* crow_t = (const float*)__builtin_assume_aligned(
+                smem + opaque(W::OFF_C + (t & 1) * W::HMAX * 4 + 4 * off), 8);
             // frame t retires output positions [t*HOP - NFFT/2, (t+1)*HOP - NFFT/2)
             // interior: every slot o and its scored clean index o + lag lie in [0, len)
             const bool edge = (t < R - 1) || (t >= nf);
@@ -630,7 +631,8 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             const bool head = want_y && lo < out_len;                      // uniform
             float inv[F];
             if (R == 2) {
-                const float* it = (const float*)(smem + opaque(W::OFF_IWS + 4 * W::ISTR * i));
+                const float* it = (const float*)__builtin_assume_aligned(
+                    smem + opaque(W::OFF_IWS + 4 * W::ISTR * i), 16);
 #pragma unroll
                 for (int q = 0; q < F; ++q) inv[q] = it[q];
             } else {

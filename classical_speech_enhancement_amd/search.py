@@ -32,6 +32,7 @@ calculate_snr.
 """
 
 import math
+import os
 from collections import OrderedDict
 
 import numpy as np
@@ -235,3 +236,48 @@ def optimize_parameters(clean_reference, noisy_audio, sr, algorithm, param_range
     return {"snr": {"score": score, "params": dict(specs[cid][2]), "cell": int(cid)},
             "baseline": {"snr": base}, "improvements": {"snr": score - base},
             "table": table}
+
+
+def run_sweep(clean, noisy, stems, out_root, sr=16000, algorithms=None, grids=None,
+              group=None, device=None):
+    """The reference's batch driver (main, speech_enhancement_comparison.py:378-474)
+    on the device: every pair x algorithm x grid cell scored after
+    finalize_enhanced, the SNR-best cell per (pair, algorithm) selected by the
+    sequential tolerance scan, its waveform written as
+    results_{alg}/{stem}_{alg}_optimized_snr.wav, and the summary files
+    (results.write_summary) under results_summary/.  Rank 0 writes."""
+    import torch.distributed as dist
+    from . import results
+    from .engine import Engine
+    grids = grids or ALGORITHM_GRIDS
+    algorithms = list(algorithms or grids)
+    specs = job_specs(len(noisy), algorithms, grids)
+    table, best = run_grid(clean, noisy, specs, group=group, device=device)
+    rank = dist.get_rank(group) if (dist.is_available() and dist.is_initialized()) else 0
+    if rank != 0:
+        return None
+    eng = Engine()
+    rows = []
+    for pair, stem in enumerate(stems):
+        c = np.asarray(clean[pair], np.float64)
+        n = np.asarray(noisy[pair], np.float64)
+        m = min(len(c), len(n))
+        err = np.sum((c[:m] - n[:m]) ** 2)
+        snr_noisy = math.inf if err == 0 else float(10 * np.log10(np.sum(c[:m] ** 2) / (err + 1e-10)))
+        for alg in algorithms:
+            cid, score = best[(pair, alg)]
+            if cid < 0:
+                raise ValueError(f"Optimization failed for snr - no valid parameters found! ({stem}, {alg})")
+            params = specs[cid][2]
+            import torch
+            x = torch.as_tensor(n).cuda().view(1, -1)
+            cl = torch.as_tensor(c).cuda().view(1, -1)
+            res = eng.run(x, [(0, alg, params)], clean=cl, want_waveforms=True, align=True)
+            y = res["y"][0].double().cpu().numpy()
+            e = results.shift_and_fit(y, int(res["lag"][0]), len(c))
+            out_dir = os.path.join(out_root, f"results_{alg}")
+            os.makedirs(out_dir, exist_ok=True)
+            results.write_wav_pcm16(os.path.join(out_dir, f"{stem}_{alg}_optimized_snr.wav"), e, sr)
+            rows.append(results.result_row(stem, alg, sr, snr_noisy, float(score), params))
+    results.write_summary(rows, algorithms, os.path.join(out_root, "results_summary"))
+    return rows

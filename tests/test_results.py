@@ -1,0 +1,54 @@
+"""Results I/O in the reference's formats (speech_enhancement_comparison.py
+:267-270, :314-373, :462-471): row schema, summary means, CSV with NA, PCM16
+WAV round trip."""
+
+import json
+
+import numpy as np
+
+from classical_speech_enhancement_amd import results
+
+
+def test_row_has_every_reference_key():
+    row = results.result_row("p01", "mmse", 16000, 3.2, 7.5, {"alpha": 0.98})
+    for k in results.ROW_KEYS:
+        assert k in row
+    assert row["stoi_noisy"] is None and row["pesq_balopt"] is None
+    assert row["snr_balopt"] == 7.5 and row["best_params_snr"] == {"alpha": 0.98}
+
+
+def test_summary_csv_and_json(tmp_path):
+    rows = [results.result_row("a", "mmse", 16000, 1.0, 5.0, {}),
+            results.result_row("b", "mmse", 16000, 2.0, 7.0, {}),
+            results.result_row("a", "wiener", 16000, 1.0, 4.0, {})]
+    summary = results.write_summary(rows, ["mmse", "wiener", "omlsa"], str(tmp_path))
+    assert summary["mmse"]["count"] == 2 and summary["mmse"]["snr_balopt_mean"] == 6.0
+    assert summary["omlsa"]["count"] == 0 and summary["omlsa"]["snr_balopt_mean"] is None
+    assert summary["mmse"]["stoi_noisy_mean"] is None
+    lines = (tmp_path / "all_results.csv").read_text().splitlines()
+    assert lines[0] == ("stem,alg,stoi_noisy,pesq_noisy,stoi_stoiopt,pesq_stoiopt,stoi_pesqopt,"
+                        "pesq_pesqopt,stoi_balopt,pesq_balopt,snr_balopt")
+    assert lines[1] == "a,mmse,NA,NA,NA,NA,NA,NA,NA,NA,5.0000"
+    back = json.loads((tmp_path / "all_results.json").read_text())
+    assert back[2]["alg"] == "wiener"
+    assert json.loads((tmp_path / "summary_means.json").read_text())["wiener"]["count"] == 1
+
+
+def test_wav_pcm16_round_trip(tmp_path):
+    x = np.array([0.0, 0.5, -0.5, 1.0, -1.0, 0.25 / 32767, 0.9999], dtype=np.float64)
+    p = str(tmp_path / "x.wav")
+    results.write_wav_pcm16(p, x, 16000)
+    y, sr = results.read_wav_pcm16(p)
+    assert sr == 16000 and len(y) == len(x)
+    q = np.rint(x.astype(np.float32).astype(np.float64) * 32767).astype(int)
+    np.testing.assert_array_equal(np.rint(y * 32768).astype(int), q)
+
+
+def test_shift_and_fit_matches_oracle_finalize():
+    import oracle
+    rng = np.random.default_rng(0)
+    y = rng.normal(0, 0.5, 1000)
+    for lag in (-7, 0, 5):
+        e = results.shift_and_fit(y, lag, 990)
+        ref = np.clip(oracle.match_length(oracle.pipeline_ref.shift_by_lag(y, lag), 990), -1, 1)
+        np.testing.assert_array_equal(e, ref)
