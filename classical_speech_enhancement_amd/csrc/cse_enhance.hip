@@ -199,6 +199,20 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 // into LDS once, cooperatively, one frame ahead (a few VGPRs per thread),
 // instead of every lane keeping 17 bins of loads in flight.
 // ---------------------------------------------------------------------------
+// CSE_DIRECT_ROWS=1: every lane loads its own Y/N bins from global memory
+// (L1/L2-resident: the 12 cells of a workgroup read the same rows) one frame
+// ahead into registers, and each wave stages its own clean row in LDS, so the
+// frame loop has no workgroup barrier.  0: the workgroup stages shared Y/N/C
+// rows in LDS, one barrier per frame.
+#ifndef CSE_DIRECT_ROWS
+#define CSE_DIRECT_ROWS 0  // r01: 1 measured equal (31.3 vs 31.0 ms at 8 pairs, 92 B spill)
+#endif
+// where the next frame's Y/N loads are issued: 0 after the gain stage,
+// 1 after the transpose, 2 before the retire
+#ifndef CSE_PREFETCH_AT
+#define CSE_PREFETCH_AT 0
+#endif
+
 template <int NFFT>
 struct WG {
     using G = Geo<NFFT>;
@@ -216,9 +230,10 @@ struct WG {
     static constexpr int YROW = ((G::B * 8 + 15) / 16) * 16;      // bytes of one Y row
     static constexpr int NROW = ((G::B * 4 + 15) / 16) * 16;      // bytes of one N row
     static constexpr int OFF_Y = CPWG * CREG;                     // float2[2][B] (double buffer)
-    static constexpr int OFF_N = OFF_Y + 2 * YROW;                // float[2][B]
-    static constexpr int OFF_C = OFF_N + 2 * NROW;                // float[2][HMAX]
-    static constexpr int OFF_TW = OFF_C + 2 * HMAX * 4;           // cf[15][L] (b = 1..15)
+    static constexpr int OFF_N = OFF_Y + (CSE_DIRECT_ROWS ? 0 : 2 * YROW);  // float[2][B]
+    static constexpr int OFF_C = OFF_N + (CSE_DIRECT_ROWS ? 0 : 2 * NROW);  // float[(waves)][2][HMAX]
+    static constexpr int CBUF = 2 * HMAX * 4;                     // one clean double buffer
+    static constexpr int OFF_TW = OFF_C + (CSE_DIRECT_ROWS ? WAVES : 1) * CBUF;  // cf[15][L]
     static constexpr int OFF_LC = OFF_TW + 15 * G::L * 8;         // cf[L] packing rotor
     static constexpr int OFF_CP = OFF_LC + G::L * 8;              // float[CPWG][8] cell params
     // synthesis window w(n)/NFFT at the lane's 32 sample slots; row stride 36
@@ -343,6 +358,25 @@ __device__ __forceinline__ void gain_row(const float2* __restrict__ yr, const fl
     }
 }
 
+// gain_row with the frame's bins already in registers (CSE_DIRECT_ROWS)
+template <int NFFT, int ALGO, bool OUT>
+__device__ __forceinline__ void gain_row_regs(const float2 (&y)[17], const float (&n)[17],
+                                              cf* __restrict__ sb, float (&rr)[17], float alpha_t,
+                                              const CellParam& cpar, float* __restrict__ grow,
+                                              int i) {
+    constexpr int L = Geo<NFFT>::L, M = Geo<NFFT>::M;
+#pragma unroll
+    for (int j = 0; j < 17; ++j) {
+        const int kk = (j < 16) ? L * j : M;
+        float g;
+        const cf Sj = gain_bin<ALGO>(y[j], n[j], rr[j], alpha_t, cpar, g);
+        if (j < 16 || i == 0) {
+            sb[kk] = Sj;
+            if (OUT && grow) grow[kk] = g;
+        }
+    }
+}
+
 template <int NFFT, int HOP, int ALGO, bool OUT>
 __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, int n_cells_wg,
                                        unsigned char* smem) {
@@ -425,6 +459,49 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         ((CellParam*)(smem + W::OFF_CP))[c] = prm;
     }
 
+#if CSE_DIRECT_ROWS
+    // ---- per-lane Y/N bins of frame t in registers (loaded one frame ahead);
+    // lanes other than 0 load the Nyquist bin too (same address, discarded)
+    float2 yv[17];
+    float nv[17];
+    auto load_yn = [&](int t) {
+        const float2* yt = Ybase + (int64_t)t * B;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) yv[j] = yt[i + L * j];
+        yv[16] = yt[M];
+        if (nstride || t == 0) {  // a static noise row is loaded once
+            const float* nt = Nbase + (int64_t)t * nstride;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) nv[j] = nt[i + L * j];
+            nv[16] = nt[M];
+        }
+    };
+    // ---- per-wave clean rows (double-buffered, wave-private: no barrier)
+    constexpr int CPL = W::HMAX / 64;
+    double pcd[CPL];
+    float* cwave = (float*)(smem + W::OFF_C + wave * W::CBUF);
+    auto load_c = [&](int t) {
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const int j = lane + 64 * u;
+            const int o = t * HOP - NFFT / 2 + j + lag;  // clean sample scored against y[o - lag]
+            pcd[u] = (j < HOP && cbase && o >= 0 && o < len) ? cbase[o] : 0.0;
+        }
+    };
+    auto store_c = [&](int t) {
+        float* crow = cwave + (t & 1) * W::HMAX;
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const int j = lane + 64 * u;
+            if (j < HOP) crow[j] = (float)pcd[u];
+        }
+    };
+    load_yn(0);
+    load_c(0);
+    store_c(0);
+    load_c(1);
+    __syncthreads();  // workgroup tables written
+#else
     // ---- row staging: thread tid owns Y/N elements tid + u*THREADS, clean tid + u*THREADS
     float2 py[W::YPT];
     float pn[W::YPT];
@@ -478,6 +555,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     load_rows(0);
     store_rows(0);
     load_rows(1);
+#endif
 
     const int b2 = (L == 16) ? i : (i & 15);
     const int h2 = (L == 16) ? 0 : (i >> 4);
@@ -495,9 +573,11 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     for (int t = 0; t < nf + R - 1; ++t) {
         float x[32];  // this frame's windowed IFFT samples (0 in flush frames)
         if (t < nf) {
+#if !CSE_DIRECT_ROWS
             // the one workgroup barrier per frame: rows(t) (stored during frame
             // t-1) are visible, and nobody still reads buffer (t+1)&1
             if (!(CSE_ABLATE & 8)) __syncthreads();
+#endif
             CSE_MARK("gain");
             // ---------------- gain stage: S = Y * G into my cell's LDS row
             {
@@ -505,6 +585,12 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     *(const CellParam*)(smem + opaque(W::OFF_CP + 32 * cslot));
                 const float alpha_t = (t == 0) ? 0.0f : cpar.p0;  // see gain_wiener
                 cf* sb = (cf*)(smem + opaque(creg + 8 * i));   // &S[i]
+#if CSE_DIRECT_ROWS
+                gain_row_regs<NFFT, ALGO, OUT>(yv, nv, sb, rr, alpha_t, cpar,
+                                               (OUT && gout) ? gout + t * B + i : nullptr, i);
+            }
+            if (CSE_PREFETCH_AT == 0 && t + 1 < nf) load_yn(t + 1);  // in flight during the IFFT
+#else
                 const float2* yr =
                     (const float2*)(smem + opaque(W::OFF_Y + (t & 1) * W::YROW + 8 * i));
                 const float* nr =
@@ -512,11 +598,14 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 gain_row<NFFT, ALGO, OUT>(yr, nr, sb, rr, alpha_t, cpar,
                                           (OUT && gout) ? gout + t * B + i : nullptr, i);
             }
+#endif
             CSE_MARK("rows");
+#if !CSE_DIRECT_ROWS
             if (!(CSE_ABLATE & 64)) {
                 store_rows(t + 1);  // other buffer: its last readers passed this frame's barrier
                 load_rows(t + 2);
             }
+#endif
             wave_sync();  // my wave's S rows complete (cells never span waves)
 
             CSE_MARK("pass1");
@@ -567,6 +656,9 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     if (!(CSE_ABLATE & 128)) tw_[b * TR] = z[b];
             }
             wave_sync();  // transpose block written
+#if CSE_DIRECT_ROWS
+            if (CSE_PREFETCH_AT == 1 && t + 1 < nf) load_yn(t + 1);
+#endif
 
             CSE_MARK("pass2");
             // ---------------- pass 2: DFT over the lane index --------------
@@ -599,13 +691,18 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 for (int q = 0; q < 32; ++q) x[q] = ((q & 1) ? v[q >> 1].y : v[q >> 1].x) * wt[q];
             }
         } else {
+#if !CSE_DIRECT_ROWS
             __syncthreads();  // flush frames: clean row t visible, row t-1 reads done
             store_rows(t + 1);
             load_rows(t + 2);
+#endif
 #pragma unroll
             for (int q = 0; q < 32; ++q) x[q] = 0.0f;
         }
 
+#if CSE_DIRECT_ROWS
+        if (CSE_PREFETCH_AT == 2 && t + 1 < nf) load_yn(t + 1);
+#endif
         CSE_MARK("retire");
         // ---------------- overlap-add + retire HOP finished samples ---------
         // slot q < F of this frame completes output position t*HOP + n(q):
@@ -620,8 +717,13 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         for (int q = 0; q < PEND; ++q) acc[q] = (q + F < PEND ? acc[q + F] : 0.0f) + x[q + F];
         if (valid && !(CSE_ABLATE & 4)) {
             const int o0 = t * HOP + off - NFFT / 2;  // output index of q = 0
+#if CSE_DIRECT_ROWS
+            const float* crow_t = (const float*)__builtin_assume_aligned(
+                smem + opaque(W::OFF_C + wave * W::CBUF + (t & 1) * W::HMAX * 4 + 4 * off), 8);
+#else
             const float* crow_t = (const float*)__builtin_assume_aligned(
                 smem + opaque(W::OFF_C + (t & 1) * W::HMAX * 4 + 4 * off), 8);
+#endif
             // frame t retires output positions [t*HOP - NFFT/2, (t+1)*HOP - NFFT/2)
             // interior: every slot o and its scored clean index o + lag lie in [0, len)
             const bool edge = (t < R - 1) || (t >= nf);
@@ -687,6 +789,10 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 #pragma unroll
             for (int q = 0; q < F; ++q) asm volatile("" ::"v"(done[q]));
         }
+#if CSE_DIRECT_ROWS
+        store_c(t + 1);  // buffer (t+1)&1: this wave's last read of it was frame t-1
+        load_c(t + 2);
+#endif
         CSE_MARK("end");
     }
 

@@ -245,27 +245,39 @@ __global__ void finish_kernel(const cse_noise_job_t* __restrict__ jobs, int B,
     const float* Ns = src + jb.src_offset + sig * (int64_t)jb.src_frames * B + b;
     float* Os = dst + jb.dst_offset + sig * (int64_t)jb.out_frames * B + b;
     const double mu = jb.mu, c = 1.0 - mu, ie = jb.inv_eps;
+    // 1/max(v, eps) in fp32 (correctly rounded 1/x of the rounded operand:
+    // within 1.5 ulp of the fp64 quotient, which the f32 row stores anyway);
+    // the fp64 divide made this launch latency-bound
+    const float ief = (float)ie;
     auto put = [&](int t, double v) {
-        Os[(int64_t)t * B] = ie > 0.0 ? (float)(1.0 / fmax(v, ie)) : (float)v;
+        Os[(int64_t)t * B] = ie > 0.0 ? 1.0f / fmaxf((float)v, ief) : (float)v;
     };
     double s = (double)Ns[0];
     put(0, s);
-    int t = 1;
-    for (; t + 8 <= jb.out_frames; t += 8) {
-        double x[8];
+    // software-pipelined: the loads of block k+1 are in flight while block k's
+    // serial recurrence runs (a dependent chain per (signal, bin))
+    constexpr int U = 16;
+    const int nfr = jb.out_frames, nsrc = jb.src_frames;
+    auto fetch = [&](int t0, float (&xs)[U]) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            x[u] = (t + u) < jb.src_frames ? (double)Ns[(int64_t)(t + u) * B] : 0.0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            s = __dadd_rn(__dmul_rn(mu, s), __dmul_rn(c, x[u]));
-            put(t + u, s);
+        for (int u = 0; u < U; ++u) {
+            const int tt = t0 + u;
+            xs[u] = (tt < nsrc && tt < nfr) ? Ns[(int64_t)tt * B] : 0.0f;
         }
-    }
-    for (; t < jb.out_frames; ++t) {
-        const double x = t < jb.src_frames ? (double)Ns[(int64_t)t * B] : 0.0;
-        s = __dadd_rn(__dmul_rn(mu, s), __dmul_rn(c, x));
-        put(t, s);
+    };
+    float cur[U], nxt[U];
+    fetch(1, cur);
+    for (int t = 1; t < nfr; t += U) {
+        fetch(t + U, nxt);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (t + u < nfr) {
+                s = __dadd_rn(__dmul_rn(mu, s), __dmul_rn(c, (double)cur[u]));
+                put(t + u, s);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
     }
 }
 
