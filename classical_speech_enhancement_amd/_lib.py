@@ -31,7 +31,8 @@ NOISE_JOB_DTYPE = np.dtype([
     ("out_frames", np.int32), ("mu", np.float64), ("inv_eps", np.float64)], align=True)
 assert NOISE_JOB_DTYPE.itemsize == 40
 
-EXPORTS = ("cse_version", "cse_last_error", "cse_stft", "cse_noise_workspace_bytes",
+EXPORTS = ("cse_version", "cse_last_error", "cse_cells_per_group", "cse_stft",
+           "cse_noise_workspace_bytes",
            "cse_noise_estimate", "cse_noise_smooth", "cse_noise_median",
            "cse_noise_percentile_med", "cse_noise_min_tracking_med", "cse_noise_finish",
            "cse_noise_invert", "cse_istft_norm", "cse_enhance_cells",
@@ -40,8 +41,11 @@ XCORR_OK, XCORR_AMBIGUOUS, XCORR_NONFINITE = 0, 1, 2
 
 
 def cells_per_group(n_fft):
-    """Cells per workgroup slot group (CSE_CELLS_PER_GROUP)."""
-    return 12 if n_fft == 512 else 6
+    """Cells per workgroup slot group (CSE_CELLS_PER_GROUP of the loaded build)."""
+    n = int(load().cse_cells_per_group(int(n_fft)))
+    if n <= 0:
+        raise CseError(f"n_fft={n_fft} not supported")
+    return n
 
 
 class CseError(RuntimeError):
@@ -65,6 +69,8 @@ def load(path=LIB_PATH):
     lib.cse_version.argtypes = []
     lib.cse_last_error.restype = ctypes.c_char_p
     lib.cse_last_error.argtypes = []
+    lib.cse_cells_per_group.restype = i32
+    lib.cse_cells_per_group.argtypes = [i32]
     lib.cse_stft.restype = i32
     lib.cse_stft.argtypes = [P, P, i64, i64, i32, i32, P, P, P]
     lib.cse_noise_workspace_bytes.restype = i64

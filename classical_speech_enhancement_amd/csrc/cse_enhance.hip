@@ -216,7 +216,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 template <int NFFT>
 struct WG {
     using G = Geo<NFFT>;
-    static constexpr int WAVES = 3;
+    static constexpr int WAVES = CSE_WG_WAVES;
     static constexpr int THREADS = 64 * WAVES;
     static constexpr int CPWG = WAVES * G::CPW;                   // cells per workgroup
     static constexpr int HMAX = 256;                              // largest hop
@@ -248,8 +248,11 @@ struct WG {
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
-static_assert(WG<512>::BYTES <= 163840 / 4, "n_fft=512 workgroup must fit 4 per CU");
-static_assert(WG<1024>::BYTES <= 163840 / 3, "n_fft=1024 workgroup must fit 3 per CU");
+// LDS decides how many workgroups share a CU: keep >= 12 waves (3 per SIMD)
+static_assert((163840 / WG<512>::BYTES) * CSE_WG_WAVES >= 12,
+              "n_fft=512 workgroups must fill 12 waves per CU");
+static_assert((163840 / WG<1024>::BYTES) * CSE_WG_WAVES >= 8,
+              "n_fft=1024 workgroups must fill 8 waves per CU");
 static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
               WG<1024>::CPWG == CSE_CELLS_PER_GROUP(1024), "cse.h slot-group size");
 
@@ -844,6 +847,10 @@ __global__ void __launch_bounds__(WG<NFFT>::THREADS, CSE_WAVES_PER_SIMD) enhance
 }  // namespace cse
 
 using namespace cse;
+
+extern "C" int cse_cells_per_group(int n_fft) {
+    return (n_fft == 512 || n_fft == 1024) ? CSE_CELLS_PER_GROUP(n_fft) : 0;
+}
 
 extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
                                  const float* Y, const float* noise, const double* clean,

@@ -60,8 +60,8 @@ enum {
 
 /*
  * One grid cell = one (signal group, noise PSD, algorithm, parameter set).
- * Cells are processed CSE_CELLS_PER_GROUP(n_fft) at a time by one 192-thread
- * workgroup (3 wavefronts) that stages their shared rows in LDS, so the cells
+ * Cells are processed CSE_CELLS_PER_GROUP(n_fft) at a time by one workgroup of
+ * CSE_WG_WAVES wavefronts (4: 256 threads) that stages their shared rows in LDS, so the cells
  * of one such slot group (cells[g*G .. g*G+G-1]) MUST share algo, hop,
  * y_offset, noise_offset, noise_stride, clean_offset and lag; pad a short
  * group with CSE_ALGO_NONE slots.  Only param, out_offset and gain_offset may
@@ -85,11 +85,16 @@ typedef struct cse_cell {
     float param[8];        /* algorithm parameters, order as in the CSE_ALGO_* comments */
 } cse_cell_t;              /* 96 bytes */
 
-#define CSE_CELLS_PER_GROUP(n_fft) ((n_fft) == 512 ? 12 : 6)
+#ifndef CSE_WG_WAVES
+#define CSE_WG_WAVES 4 /* wavefronts per workgroup of the build (cse_cells_per_group reports it) */
+#endif
+#define CSE_CELLS_PER_GROUP(n_fft) ((n_fft) == 512 ? 4 * CSE_WG_WAVES : 2 * CSE_WG_WAVES)
 
 /* Library identity. */
 int cse_version(void);
 const char* cse_last_error(void);
+/* CSE_CELLS_PER_GROUP(n_fft) of this build (0 for an unsupported n_fft). */
+int cse_cells_per_group(int n_fft);
 
 /*
  * Centred, reflect-padded, periodic-Hann STFT (librosa 0.11 `stft` as called
