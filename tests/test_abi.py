@@ -48,6 +48,15 @@ def test_version_and_error_channel(lib):
     assert rc == -1 and b"Unbekannte Methode" in lib.cse_last_error()
 
 
+def test_cells_per_group_matches_header(lib):
+    import re
+    text = open(HEADER).read()
+    waves = int(re.search(r"#define CSE_WG_WAVES (\d+)", text).group(1))
+    assert lib.cse_cells_per_group(512) == _lib.cells_per_group(512) == 4 * waves
+    assert lib.cse_cells_per_group(1024) == 2 * waves
+    assert lib.cse_cells_per_group(256) == 0
+
+
 def test_cell_struct_layout():
     assert _lib.CELL_DTYPE.itemsize == 96
     off = {n: _lib.CELL_DTYPE.fields[n][1] for n in _lib.CELL_DTYPE.names}

@@ -42,3 +42,31 @@ def test_run_sweep_files_and_selection(tmp_path):
     summ = os.path.join(tmp_path, "results_summary")
     for f in ("all_results.json", "summary_means.json", "all_results.csv"):
         assert os.path.exists(os.path.join(summ, f))
+
+
+def test_prepare_pair_matches_oracle():
+    """prepare_pair (speech_enhancement_comparison.py:71-90): mono, 48 k -> 16 k,
+    trim, device alignment of a delayed noisy copy == the oracle's
+    align_to_reference on the same resampled arrays."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from scipy.signal import resample_poly
+    from classical_speech_enhancement_amd import prepare
+    from classical_speech_enhancement_amd.synth import make_pair
+    c16, n16 = make_pair(21, 3.0)
+    c48 = resample_poly(c16, 3, 1)
+    for delay in (0, 37, -123):
+        n48 = resample_poly(np.roll(n16, delay), 3, 1)
+        stereo = np.stack([n48, 0.5 * n48], axis=1)  # (samples, 2): averaged like to_mono
+        cl, nz, sr = prepare.prepare_pair(c48, 48000, stereo, 48000)
+        rc = resample_poly(c48, 1, 3)
+        rn = resample_poly(oracle.to_mono(stereo), 1, 3)
+        L = min(len(rc), len(rn))
+        rc, rn = rc[:L], rn[:L]
+        ref = oracle.match_length(oracle.align_to_reference(rc, rn, 16000), L)
+        assert sr == 16000
+        np.testing.assert_array_equal(cl, rc)
+        np.testing.assert_array_equal(nz, ref)
+        lag = oracle.align_lag(rc, rn, 16000)
+        assert lag == prepare.alignment_lag(rc, rn, 16000)
