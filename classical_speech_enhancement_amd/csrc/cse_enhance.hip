@@ -183,13 +183,34 @@ __device__ __forceinline__ float gain_omlsa(float P, float inv, float& rr, float
 }
 
 // ---------------------------------------------------------------------------
-// XCD-aware wave order: blocks are dealt round-robin over the 8 XCDs, so give
-// each XCD a contiguous slice of the (cost-sorted, group-clustered) cell list.
+// Block -> slot-group order.  Blocks are dealt round-robin over the 8 XCDs
+// (block b runs on XCD b % 8, as its (b/8)-th block there), and the host sorts
+// slot groups longest-first with groups that share rows adjacent.
+//   CSE_XCD_MAP 0: identity (XCDs interleave group by group)
+//   CSE_XCD_MAP 1: each XCD a contiguous slice (best L2 reuse, but XCD 0 gets
+//                  all the longest groups)
+//   CSE_XCD_MAP 2: runs of CSE_XCD_RUN consecutive groups per XCD, the runs
+//                  dealt round-robin: L2 reuse inside a run, balanced XCDs
 // ---------------------------------------------------------------------------
+#ifndef CSE_XCD_MAP
+#define CSE_XCD_MAP 2
+#endif
+#ifndef CSE_XCD_RUN
+#define CSE_XCD_RUN 4
+#endif
 __device__ __forceinline__ int xcd_remap(int b, int nb) {
-    const int q = nb / 8, r = nb % 8;
+    if (CSE_XCD_MAP == 0) return b;
     const int xcd = b % 8, idx = b / 8;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+    if (CSE_XCD_MAP == 1) {
+        const int q = nb / 8, r = nb % 8;
+        return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+    }
+    // runs: chunk k (k = idx / RUN) of XCD x covers groups [(k*8 + x)*RUN, +RUN)
+    constexpr int RUN = CSE_XCD_RUN;
+    const int g = ((idx / RUN) * 8 + xcd) * RUN + idx % RUN;
+    // the tail (nb not a multiple of 8*RUN) falls back to the identity order
+    const int full = (nb / (8 * RUN)) * (8 * RUN);
+    return b < full ? g : b;
 }
 
 // ---------------------------------------------------------------------------
