@@ -78,6 +78,17 @@ __device__ __forceinline__ float estrin_rec(const float (&c)[K], const float (&p
 #else
 #define CSE_MARK(name)
 #endif
+// CSE_PRIO: bit 1 raises the wave's issue priority (s_setprio) over the gain
+// stage, so a wave in its VALU-dense stage is issued ahead of waves in their
+// LDS-bound IFFT/retire stages, whose latency then overlaps it
+// (13 pairs: 33.3 -> 31.5 ms).  Bits 2 and 4 (priority over the IFFT passes)
+// measured slower.
+#ifndef CSE_PRIO
+#define CSE_PRIO 1
+#endif
+#ifndef CSE_PRIO_LEVEL
+#define CSE_PRIO_LEVEL 1
+#endif
 #ifndef CSE_ESTRIN
 #define CSE_ESTRIN 0
 #endif
@@ -603,6 +614,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             if (!(CSE_ABLATE & 8)) __syncthreads();
 #endif
             CSE_MARK("gain");
+            if (CSE_PRIO & 1) __builtin_amdgcn_s_setprio(CSE_PRIO_LEVEL);
             // ---------------- gain stage: S = Y * G into my cell's LDS row
             {
                 const CellParam cpar =
@@ -624,6 +636,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             }
 #endif
             CSE_MARK("rows");
+            if (CSE_PRIO & 1) __builtin_amdgcn_s_setprio(0);
 #if !CSE_DIRECT_ROWS
             if (!(CSE_ABLATE & 64)) {
                 store_rows(t + 1);  // other buffer: its last readers passed this frame's barrier
@@ -633,6 +646,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             wave_sync();  // my wave's S rows complete (cells never span waves)
 
             CSE_MARK("pass1");
+            if (CSE_PRIO & 2) __builtin_amdgcn_s_setprio(1);
             // ---------------- pass 1: real-IFFT packing + DFT16 over j -----
             // Z'[k] = (X_k + X*_{M-k}) + i (X_k - X*_{M-k}) e^{2πi k/NFFT}
             cf z[16];
@@ -685,6 +699,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 #endif
 
             CSE_MARK("pass2");
+            if (CSE_PRIO & 4) __builtin_amdgcn_s_setprio(1);
             // ---------------- pass 2: DFT over the lane index --------------
             cf v[16];
             {
@@ -727,6 +742,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 #if CSE_DIRECT_ROWS
         if (CSE_PREFETCH_AT == 2 && t + 1 < nf) load_yn(t + 1);
 #endif
+        if (CSE_PRIO & 6) __builtin_amdgcn_s_setprio(0);
         CSE_MARK("retire");
         // ---------------- overlap-add + retire HOP finished samples ---------
         // slot q < F of this frame completes output position t*HOP + n(q):
