@@ -150,7 +150,7 @@ def main():
     pairs = [make_pair(rank * P + i, args.seconds) for i in range(P)]
     clean = torch.as_tensor(np.stack([c for c, _ in pairs])).cuda()
     noisy = torch.as_tensor(np.stack([n for _, n in pairs])).cuda()
-    clean_pow = (clean ** 2).sum(dim=1).cpu().numpy()
+    clean_pow = np.array([float(np.dot(c, c)) for c, _ in pairs])
     L = noisy.shape[1]
     specs = grid_specs(P, 512)
     # Two plans, double-buffered: the next step's STFT + noise PSDs run on a

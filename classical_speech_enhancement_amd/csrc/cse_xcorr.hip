@@ -6,8 +6,8 @@
 // and lag = the first l of maximal c (np.argmax over ascending lags, :60).
 //
 // Blocked FFT correlation.  The output head e[0, n) is cut into blocks of
-// XB = 4096 samples; block b correlates with the clean window
-// r0[bXB - max_lag, bXB + XB + max_lag) (7296 <= XN = 8192 samples, so the
+// XB = 4992 samples (7 blocks for 2 s at 16 kHz); block b correlates with the
+// clean window r0[bXB - max_lag, bXB + XB + max_lag) (<= XN = 8192 samples, so the
 // circular correlation of length XN has no wrap-around in the kept lags):
 //   C(f) = sum_b R_b(f) conj(S_b(f)),   c_raw = irfft(C) on lags 0..2 max_lag,
 // one inverse transform per cell.  R_b (the clean side) is computed once per
@@ -29,7 +29,7 @@ namespace cse {
 
 constexpr int XN = 8192;      // real transform length of one block correlation
 constexpr int XH = XN / 2;    // complex FFT length
-constexpr int XB = 4096;      // output samples per block
+constexpr int XB = XN - 2 * 1600;  // output samples per block: the 0.1-s lags of 16 kHz fill XN
 constexpr int XT = 256;       // threads per workgroup
 constexpr int XCAND = 64;     // candidates re-evaluated in fp64
 #ifndef CSE_XC_WG_PER_CU

@@ -126,7 +126,8 @@ def engine_compute(clean, noisy, specs, ids, engine=None, align=True):
         cl = torch.as_tensor(np.stack([np.asarray(clean[p], np.float64) for p in pairs])).cuda()
         sub = [(slot[specs[ids[j]][0]], specs[ids[j]][1], specs[ids[j]][2]) for j in js]
         res = eng.run(nz, sub, clean=cl, align=align)
-        cpow = (cl ** 2).sum(dim=1).cpu().numpy()
+        cpow = np.array([float(np.dot(np.asarray(clean[p], np.float64),
+                                      np.asarray(clean[p], np.float64))) for p in pairs])
         snr = snr_db(res["sse"], cpow[[s for (s, _, _) in sub]])
         out[js, 0] = res["sse"]
         out[js, 1] = snr

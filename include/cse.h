@@ -223,7 +223,7 @@ int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n
  * enhanced output (s0); the first maximum in ascending lag order (np.argmax,
  * :60).  The reference uses n = min(len, 2 s * sr) and max_lag = 0.1 s * sr and
  * skips alignment when n < 256 (:44-46) — the caller applies those rules.
- * Requires max_lag <= 2048.
+ * Requires max_lag <= 1600 (0.1 s at 16 kHz).
  *
  * cse_xcorr_prepare: per-signal tables (FFT blocks of the clean reference,
  *   fp64 r0, overlap sums, zero-padding energies) into the workspace of
