@@ -57,7 +57,7 @@ def _single(alg, noisy, clean, params, rule):
             raise NotImplementedError("true_noise with clean shorter than noisy (frame edge-pad)")
     res = eng.run(_dev(x), [(0, alg, params)], clean=None if c is None else _dev(c),
                   want_waveforms=True)
-    return res["y"][0].double().cpu().numpy()
+    return res["y"][0].cpu().numpy().astype(np.float64)
 
 
 def spectral_subtraction(noisy_audio, sr, alpha, beta, n_fft, hop_length, noise_percentile,
@@ -113,14 +113,15 @@ def noise_estimation(y, sr, method="percentile", n_fft=1024, hop_length=256, win
     T = n_frames(len(x), hop_length)
     if T < 5:
         _, P = eng.stft(xd, n_fft, hop_length, want_y=False)
-        return eng.noise_estimate("percentile", P, 25.0, eps)[0].double().cpu().numpy()[:, None]
+        N = eng.noise_estimate("percentile", P, 25.0, eps)
+        return N[0].cpu().numpy().astype(np.float64)[:, None]
     if method == "percentile":
         _, P = eng.stft(xd, n_fft, hop_length, want_y=False)
         N = eng.noise_estimate("percentile", P, params.get("percentile", 20.0), eps)
-        return N[0].double().cpu().numpy()[:, None]
+        return N[0].cpu().numpy().astype(np.float64)[:, None]
     if method == "min_tracking":
         _, P = eng.stft(xd, n_fft, hop_length, want_y=False)
-        return eng.noise_estimate("min_tracking", P, eps=eps)[0].double().cpu().numpy().T
+        return eng.noise_estimate("min_tracking", P, eps=eps)[0].cpu().numpy().astype(np.float64).T
     if method == "true_noise":
         clean = params.get("clean_audio")
         if clean is None:
@@ -130,5 +131,5 @@ def noise_estimation(y, sr, method="percentile", n_fft=1024, hop_length=256, win
         c[:m] = np.asarray(clean, dtype=np.float64)[:m]
         _, P = eng.stft(xd, n_fft, hop_length, x_sub=_dev(c), want_y=False)
         out = eng.noise_estimate("true_noise", P, eps=params.get("eps", 1e-12))
-        return out[0].double().cpu().numpy().T
+        return out[0].cpu().numpy().astype(np.float64).T
     raise ValueError(f"Unbekannte Methode: {method}")

@@ -274,7 +274,7 @@ def run_sweep(clean, noisy, stems, out_root, sr=16000, algorithms=None, grids=No
             x = torch.as_tensor(n).cuda().view(1, -1)
             cl = torch.as_tensor(c).cuda().view(1, -1)
             res = eng.run(x, [(0, alg, params)], clean=cl, want_waveforms=True, align=True)
-            y = res["y"][0].double().cpu().numpy()
+            y = res["y"][0].cpu().numpy().astype(np.float64)
             e = results.shift_and_fit(y, int(res["lag"][0]), len(c))
             out_dir = os.path.join(out_root, f"results_{alg}")
             os.makedirs(out_dir, exist_ok=True)
