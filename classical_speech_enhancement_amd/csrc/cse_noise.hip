@@ -15,7 +15,7 @@
 
 namespace cse {
 
-constexpr int kMaxSortFrames = 8192;  // LDS bitonic sort capacity (T <= 8192)
+constexpr int kMaxSortFrames = 16384;  // LDS bitonic sort capacity: 128 KiB of doubles
 
 __device__ __forceinline__ bool key_less(double a, int ia, double b, int ib) {
     return a < b || (a == b && ia < ib);
@@ -94,20 +94,57 @@ __global__ void frame_energy_kernel(const double* __restrict__ P, int T, int B, 
     if (threadIdx.x == 0) energy[sig * T + t] = part[0] / (double)B;
 }
 
-// k quietest frames: argsort(energy)[:k] (ties by frame index)
+// k quietest frames: argsort(energy)[:k], ties by frame index.  Only the
+// energies are sorted (8 B per frame of LDS, so T <= kMaxSortFrames fits);
+// the index set is then recovered exactly: every frame below the k-th
+// smallest energy thr, plus the lowest-index frames equal to thr.  The output
+// order is frame order (the percentile that consumes it sorts the values).
 __global__ void select_quiet_kernel(const double* __restrict__ energy, int T, int n2, int k,
                                     int* __restrict__ sel) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double* key = (double*)smem;
-    int* idx = (int*)(key + n2);
     const int64_t sig = blockIdx.x;
-    for (int i = threadIdx.x; i < n2; i += blockDim.x) {
-        key[i] = i < T ? energy[sig * T + i] : INFINITY;
-        idx[i] = i;
-    }
+    const double* e = energy + sig * T;
+    for (int i = threadIdx.x; i < n2; i += blockDim.x) key[i] = i < T ? e[i] : INFINITY;
     __syncthreads();
-    bitonic_sort(key, idx, n2);
-    for (int i = threadIdx.x; i < k; i += blockDim.x) sel[sig * (int64_t)T + i] = idx[i];
+    bitonic_sort(key, nullptr, n2);
+    const double thr = key[k - 1];
+    // each thread a contiguous chunk of frames; two block scans give every
+    // thread its share of the ties (lowest index first) and its output slot
+    int* scan = (int*)(key + n2);  // blockDim.x ints after the sort buffer
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int chunk = (T + nt - 1) / nt;
+    const int i0 = min(T, tid * chunk), i1 = min(T, i0 + chunk);
+    int lt = 0, eq = 0;
+    for (int i = i0; i < i1; ++i) {
+        const double v = e[i];
+        lt += v < thr;
+        eq += v == thr;
+    }
+    auto exclusive_scan = [&](int v) {
+        __syncthreads();
+        scan[tid] = v;
+        __syncthreads();
+        for (int d = 1; d < nt; d <<= 1) {
+            const int add = tid >= d ? scan[tid - d] : 0;
+            __syncthreads();
+            scan[tid] += add;
+            __syncthreads();
+        }
+        const int total = scan[nt - 1];
+        const int excl = scan[tid] - v;
+        __syncthreads();
+        return make_int2(excl, total);
+    };
+    const int2 eqs = exclusive_scan(eq);
+    const int2 lts = exclusive_scan(lt);
+    const int take_eq = max(0, min(eq, (k - lts.y) - eqs.x));  // ties still needed before mine
+    const int2 outs = exclusive_scan(lt + take_eq);
+    int out = outs.x, taken = 0;
+    for (int i = i0; i < i1; ++i) {
+        const double v = e[i];
+        if (v < thr || (v == thr && taken++ < take_eq)) sel[sig * (int64_t)T + out++] = i;
+    }
 }
 
 enum { STATS_MEDIAN = 0, STATS_PERCENTILE = 1, STATS_SIMPLE = 2 };
@@ -353,7 +390,8 @@ static int launch_percentile(const double* P, const double* med, int64_t n_sig, 
     hipLaunchKernelGGL(frame_energy_kernel, dim3(T, (unsigned)n_sig), dim3(256), 0, s, P, T, B,
                        eps, w.energy);
     hipLaunchKernelGGL(select_quiet_kernel, dim3((unsigned)n_sig), dim3(1024),
-                       (size_t)n2_all * 12, s, (const double*)w.energy, T, n2_all, k, w.sel);
+                       (size_t)n2_all * 8 + 1024 * 4, s, (const double*)w.energy, T, n2_all, k,
+                       w.sel);
     hipLaunchKernelGGL(bin_stats_kernel, dim3(B, (unsigned)n_sig), dim3(256),
                        (size_t)n2_sel * sizeof(double), s, P, T, B, n2_all,
                        (int)STATS_PERCENTILE, (const int*)w.sel, k, n2_sel, pct / 100.0, 0.02,
@@ -381,7 +419,7 @@ static int reserve_lds() {
     if (!lds_ready) {
         if (hipFuncSetAttribute((const void*)select_quiet_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                kMaxSortFrames * 12) != hipSuccess ||
+                                kMaxSortFrames * 8 + 1024 * 4) != hipSuccess ||
             hipFuncSetAttribute((const void*)bin_stats_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kMaxSortFrames * 8) != hipSuccess) {
