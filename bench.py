@@ -125,6 +125,8 @@ def main():
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--nfft", type=int, default=512, choices=(512, 1024),
+                    help="which half of the HEAD grid (the metric is quoted at 512)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run each step's prep and enhance back to back on one stream")
     ap.add_argument("--align", action="store_true",
@@ -152,7 +154,7 @@ def main():
     noisy = torch.as_tensor(np.stack([n for _, n in pairs])).cuda()
     clean_pow = np.array([float(np.dot(c, c)) for c, _ in pairs])
     L = noisy.shape[1]
-    specs = grid_specs(P, 512)
+    specs = grid_specs(P, args.nfft)
     # Two plans, double-buffered: the next step's STFT + noise PSDs run on a
     # side stream while this step's enhance kernel runs (no data is shared
     # between a step's prep and the previous step's enhance).
@@ -241,7 +243,8 @@ def main():
         return
     total_units = units * world * args.steps
     value = total_units / dt
-    achieved = units * BYTES_PER_UNIT_512 / (kern_ms / 1e3)
+    bytes_per_unit = 12 * (args.nfft // 2 + 1)
+    achieved = units * bytes_per_unit / (kern_ms / 1e3)
     traffic = load_traffic(units)
     res = {
         "metric": METRIC,
@@ -258,9 +261,9 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": (f"{P} x 10-s 16-kHz synthetic pairs per GPU, HEAD parameter_ranges.py "
-                         f"grid at n_fft=512 (all 4 algorithms, 4872 cells/pair, hops 128+256): "
+                         f"grid at n_fft={args.nfft} (all 4 algorithms, 4872 cells/pair, hops 128+256): "
                          f"STFT+noise PSDs+fused gain/ISTFT/SNR per cell"),
-            "pairs_per_gpu": P, "clip_s": args.seconds, "sr": 16000, "n_fft": 512,
+            "pairs_per_gpu": P, "clip_s": args.seconds, "sr": 16000, "n_fft": args.nfft,
             "cells_per_gpu": len(specs), "units_per_step_per_gpu": units,
             "parallelism": f"pairs sharded over {world} rank(s), all_gather of per-cell records",
             "finalize_alignment": bool(args.align),
@@ -268,12 +271,12 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": achieved / HBM_PEAK, "traffic": traffic,
-            "kernel": "cse::enhance_kernel<512>", "kernel_ms": kern_ms,
-            "bytes_per_unit": BYTES_PER_UNIT_512, "units_per_launch": units,
+            "kernel": f"cse::enhance_kernel<{args.nfft}>", "kernel_ms": kern_ms,
+            "bytes_per_unit": bytes_per_unit, "units_per_launch": units,
         },
     }
     if not args.no_cpu_baseline and world == 1:
-        res["cpu_baseline"] = cpu_baseline(args.cpu_budget, args.seconds)
+        res["cpu_baseline"] = cpu_baseline(args.cpu_budget, args.seconds, args.nfft)
     print(json.dumps(res))
     if world > 1:
         dist.barrier()
