@@ -36,7 +36,9 @@ EXPORTS = ("cse_version", "cse_last_error", "cse_cells_per_group", "cse_stft",
            "cse_noise_estimate", "cse_noise_smooth", "cse_noise_median",
            "cse_noise_percentile_med", "cse_noise_min_tracking_med", "cse_noise_finish",
            "cse_noise_invert", "cse_istft_norm", "cse_enhance_cells",
-           "cse_xcorr_workspace_bytes", "cse_xcorr_prepare", "cse_xcorr_lag")
+           "cse_xcorr_workspace_bytes", "cse_xcorr_prepare", "cse_xcorr_lag",
+           "cse_stoi_workspace_bytes", "cse_stoi_scratch_bytes", "cse_stoi_prepare",
+           "cse_stoi_cells")
 XCORR_OK, XCORR_AMBIGUOUS, XCORR_NONFINITE = 0, 1, 2
 
 
@@ -97,6 +99,14 @@ def load(path=LIB_PATH):
     lib.cse_xcorr_prepare.argtypes = [P, i64, i64, i32, i32, P, P]
     lib.cse_xcorr_lag.restype = i32
     lib.cse_xcorr_lag.argtypes = [P, P, P, i64, i64, i32, i32, P, P, P, P, P, P]
+    lib.cse_stoi_workspace_bytes.restype = i64
+    lib.cse_stoi_workspace_bytes.argtypes = [i64, i64]
+    lib.cse_stoi_scratch_bytes.restype = i64
+    lib.cse_stoi_scratch_bytes.argtypes = [i64, i64]
+    lib.cse_stoi_prepare.restype = i32
+    lib.cse_stoi_prepare.argtypes = [P, i64, i64, i32, P, P]
+    lib.cse_stoi_cells.restype = i32
+    lib.cse_stoi_cells.argtypes = [P, P, P, P, i64, i64, i64, i32, P, P, P, P]
     lib.cse_enhance_cells.restype = i32
     lib.cse_enhance_cells.argtypes = [i32, i64, P, i64, P, P, P, P, i64, P, P, P, P]
     _lib = lib

@@ -1,0 +1,744 @@
+// STOI (short-time objective intelligibility) of many enhanced outputs against
+// their clean references — the score the reference's sweep optimises
+// (evaluation_metrics.py:30-36: pystoi 0.4.1 `stoi(clean, enhanced, sr,
+// extended=False)`, called per grid cell at speech_enhancement_comparison.py:180
+// after finalize_enhanced :92-106).  Restated from the published algorithm
+// (Taal et al. 2011, as implemented by pystoi 0.4.1; oracle/stoi_ref.py):
+//
+//   resample 16 kHz -> 10 kHz   Octave `resample` filter (Kaiser sinc, 581 taps
+//                               at the 5x upsampled rate) through resample_poly:
+//                               e10[5q + r] = sum_k c_r[k] e[8q + k], k in [-58, 64]
+//   silent frames               256-sample MATLAB-Hann frames at hop 128 of the
+//                               CLEAN signal more than 40 dB below its loudest
+//                               are dropped in both signals; the kept frames
+//                               are overlap-added back (frame k of the kept
+//                               list lands at 128 k)
+//   STFT                        256-sample frames of that signal at hop 128,
+//                               MATLAB-Hann, 512-point rfft
+//   bands                       15 one-third-octave bands (bins [7, 219)):
+//                               env = sqrt(sum_band |X|^2)
+//   segments                    30 frames: y scaled to x's norm, clipped at
+//                               x (1 + 10^(15/20)), both mean-removed and
+//                               normalised, correlated; mean over bands and
+//                               segments.  Fewer than 30 frames -> 1e-5.
+//
+// The clean side (resampled clean in fp64, silent-frame mask, kept-frame list,
+// band envelopes and segment statistics) is prepared once per signal
+// (cse_stoi_prepare).  Per cell one workgroup (stoi_cells_kernel):
+//   phase A  blocks of 16 STFT frames: stage the needed 16-kHz samples in LDS,
+//            polyphase-resample the distinct 128-sample 10-kHz half-blocks the
+//            block's overlap-add needs (one thread = 5 outputs of one phase
+//            group, coefficients from the scalar cache), overlap-add, window,
+//            512-point real FFT as a 256-point complex DFT16 x DFT16 over 16
+//            lanes per frame (LDS transpose one component at a time), band
+//            energies -> envelope rows in a scratch buffer;
+//   phase B  tiles of 64 segments x 15 bands from LDS, one (segment, band)
+//            correlation per thread, fp64 accumulation.
+// All arithmetic is fp64, like the reference: STOI normalises every band of
+// every 30-frame segment separately, so a band that holds only a noise floor
+// turns an fp32 FFT's roundoff (~1e-7 of the frame energy) into a visible
+// score error (measured: 1e-5 STOI on a synthetic pair).  The 16-kHz cell
+// outputs themselves are f32 (the enhance kernel's output type).
+#include "cse_common.hpp"
+
+namespace cse {
+
+namespace stoi {
+constexpr int UP = 5, DOWN = 8;          // 10 kHz / 16 kHz
+constexpr int HALF_LEN = 290;            // (581 - 1) / 2
+constexpr int KLO = -58, KN = 123;       // tap span of the 5 phases: k in [-58, 64]
+constexpr int CST = 128;                 // coefficient row stride
+constexpr int FR = 256, HOP = 128;       // frames at 10 kHz
+constexpr int NBAND = 15, NSEG = 30;
+constexpr int FB = 16;                   // STFT frames per phase-A block
+constexpr int MAXD = 2 * (FB + 1);       // distinct 10-kHz half-blocks per block
+constexpr int BT = 72;                   // ints per block table: D, p[34], sa[17], sb[17]
+constexpr int SLOTS = 9;                 // half-blocks resampled per pass (9 x 27 tasks <= 256)
+constexpr int GRP = 27;                  // phase groups (5 outputs) covering one half-block
+constexpr int SROW = 43;                 // staging: 8 rows (sample mod 8) x 43 columns
+constexpr int SSTR = 8 * SROW;           // 344 floats per staged slot (>= 331 used)
+constexpr int NT = 256;                  // threads per workgroup
+constexpr double EPS = 2.220446049250313e-16; // np.finfo(float).eps
+__constant__ int BAND_EDGE[NBAND + 1] = {7, 9, 11, 14, 17, 22, 27, 34, 43, 55,
+                                         69, 87, 109, 138, 174, 219};
+}  // namespace stoi
+
+struct StoiLayout {
+    int64_t n10, F, Mmax, Jmax, NBLK;
+    int64_t coef64, meta, x10, en, kf, btab, xtob, xstat, total;
+};
+
+static inline int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+static StoiLayout stoi_layout(int64_t n_sig, int64_t len) {
+    using namespace stoi;
+    StoiLayout L;
+    L.n10 = (len * UP + DOWN - 1) / DOWN;  // resample_poly: ceil(len * up / down)
+    L.F = L.n10 >= FR ? (L.n10 - FR) / HOP + 1 : 0;
+    L.Mmax = L.F > 1 ? L.F - 1 : 0;
+    L.Jmax = L.Mmax >= NSEG ? L.Mmax - NSEG + 1 : 0;
+    L.NBLK = (L.Mmax + FB - 1) / FB;
+    int64_t o = 0;
+    L.coef64 = o; o = align256(o + 5 * CST * 8);
+    L.meta = o;   o = align256(o + n_sig * 4 * 4);
+    L.x10 = o;    o = align256(o + n_sig * L.n10 * 8);
+    L.en = o;     o = align256(o + n_sig * L.F * 8);
+    L.kf = o;     o = align256(o + n_sig * L.F * 4);
+    L.btab = o;   o = align256(o + n_sig * L.NBLK * BT * 4);
+    L.xtob = o;   o = align256(o + n_sig * L.Mmax * 16 * 8);
+    L.xstat = o;  o = align256(o + n_sig * L.Jmax * 16 * 32);
+    L.total = o;
+    return L;
+}
+
+// ---------------------------------------------------------------------------
+// prepare 1: the resampling filter (pystoi utils._resample_window_oct for
+// p = 5, q = 8, normalised to unit sum, times up = 5 as resample_poly does),
+// laid out by phase: c_r[k] = 5 hn[290 + 8r - 5k] for |8r - 5k| <= 290.
+// ---------------------------------------------------------------------------
+__device__ double bessel_i0(double x) {
+    // power series; x <= 5.7 here, 40 terms reach full double precision
+    const double q = 0.25 * x * x;
+    double term = 1.0, sum = 1.0;
+    for (int j = 1; j < 60; ++j) {
+        term *= q / ((double)j * (double)j);
+        sum += term;
+        if (term < 1e-18 * sum) break;
+    }
+    return sum;
+}
+
+__global__ void __launch_bounds__(1024) stoi_coef_kernel(double* coef64) {
+    using namespace stoi;
+    __shared__ double h[2 * HALF_LEN + 1];
+    __shared__ double red[1024];
+    const int tid = threadIdx.x;
+    const double beta = 0.1102 * (60.0 - 8.7);  // rejection 60 dB
+    const double i0b = bessel_i0(beta);
+    double part = 0.0;
+    for (int i = tid; i < 2 * HALF_LEN + 1; i += 1024) {
+        const double a = (double)HALF_LEN;
+        const double u = ((double)i - a) / a;
+        const double kais = bessel_i0(beta * sqrt(1.0 - u * u)) / i0b;
+        const double t = (double)(i - HALF_LEN);
+        const double x = t / 8.0;  // 2 * stopband_cutoff * t, cutoff = 1/16
+        const double sinc = (i == HALF_LEN) ? 1.0 : sinpi(x) / (M_PI * x);
+        h[i] = kais * (2.0 * UP / 16.0) * sinc;
+        part += h[i];
+    }
+    red[tid] = part;
+    __syncthreads();
+    for (int s = 512; s > 0; s >>= 1) {
+        if (tid < s) red[tid] += red[tid + s];
+        __syncthreads();
+    }
+    const double total = red[0];
+    for (int i = tid; i < 5 * CST; i += 1024) {
+        const int r = i / CST, kk = i % CST;
+        const int d = 8 * r - 5 * (kk + KLO);
+        double v = 0.0;
+        if (kk < KN && d >= -HALF_LEN && d <= HALF_LEN) v = UP * h[HALF_LEN + d] / total;
+        coef64[i] = v;
+    }
+}
+
+// prepare 2: clean resampled to 10 kHz in fp64; one thread per phase group
+__global__ void __launch_bounds__(256) stoi_resample_clean_kernel(const double* __restrict__ clean,
+                                                                   int64_t len, int64_t n10,
+                                                                   const double* __restrict__ coef,
+                                                                   double* __restrict__ x10) {
+    using namespace stoi;
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int sig = blockIdx.y;
+    if (5 * q >= n10) return;
+    const double* x = clean + (int64_t)sig * len;
+    double acc[5] = {0, 0, 0, 0, 0};
+    for (int kk = 0; kk < KN; ++kk) {
+        const int64_t n = 8 * q + kk + KLO;
+        const double v = (n >= 0 && n < len) ? x[n] : 0.0;
+#pragma unroll
+        for (int r = 0; r < 5; ++r) acc[r] = fma(coef[r * CST + kk], v, acc[r]);
+    }
+    double* o = x10 + (int64_t)sig * n10;
+#pragma unroll
+    for (int r = 0; r < 5; ++r)
+        if (5 * q + r < n10) o[5 * q + r] = acc[r];
+}
+
+// MATLAB hanning(256) = scipy hann(258)[1:-1]
+__device__ __forceinline__ double hann_m(int n) {
+    return 0.5 - 0.5 * cospi(2.0 * (double)(n + 1) / (double)(stoi::FR + 1));
+}
+
+// prepare 3: frame energies 20 log10(||w x_f|| + eps) in fp64 (utils.remove_silent_frames)
+__global__ void __launch_bounds__(256) stoi_energy_kernel(const double* __restrict__ x10,
+                                                           int64_t n10, int64_t F,
+                                                           double* __restrict__ en) {
+    using namespace stoi;
+    const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int sig = blockIdx.y;
+    if (f >= F) return;
+    const double* x = x10 + (int64_t)sig * n10 + f * HOP;
+    double s = 0.0;
+    for (int n = lane; n < FR; n += 64) {
+        const double v = hann_m(n) * x[n];
+        s = fma(v, v, s);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) en[(int64_t)sig * F + f] = 20.0 * log10(sqrt(s) + EPS);
+}
+
+// prepare 4 (one workgroup per signal): mask (max - 40 dB - e < 0), kept-frame
+// list, K/M/J, and the per-block tables of distinct 10-kHz half-blocks:
+// overlap-added half-block h takes w[n] e10[kf[h]] + w[128 + n] e10[kf[h-1] + 1]
+__global__ void __launch_bounds__(256) stoi_select_kernel(const double* __restrict__ en,
+                                                           int64_t F, int64_t NBLK,
+                                                           int* __restrict__ meta,
+                                                           int* __restrict__ kf_all,
+                                                           int* __restrict__ btab_all) {
+    using namespace stoi;
+    __shared__ double red[256];
+    __shared__ int cnt[256];
+    const int sig = blockIdx.x, tid = threadIdx.x;
+    const double* e = en + (int64_t)sig * F;
+    int* kf = kf_all + (int64_t)sig * F;
+    double mx = -INFINITY;
+    for (int64_t f = tid; f < F; f += 256) mx = fmax(mx, e[f]);
+    red[tid] = mx;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (tid < s) red[tid] = fmax(red[tid], red[tid + s]);
+        __syncthreads();
+    }
+    const double thr = red[0];
+    // ordered compaction, 256 frames per round
+    int K = 0;
+    for (int64_t f0 = 0; f0 < F; f0 += 256) {
+        const int64_t f = f0 + tid;
+        const int keep = (f < F) && ((thr - 40.0 - e[f]) < 0.0);
+        cnt[tid] = keep;
+        __syncthreads();
+        for (int s = 1; s < 256; s <<= 1) {  // inclusive scan
+            const int v = tid >= s ? cnt[tid - s] : 0;
+            __syncthreads();
+            cnt[tid] += v;
+            __syncthreads();
+        }
+        if (keep) kf[K + cnt[tid] - 1] = (int)f;
+        K += cnt[255];
+        __syncthreads();
+    }
+    const int M = K > 1 ? K - 1 : 0;
+    const int J = M >= NSEG ? M - NSEG + 1 : 0;
+    if (tid == 0) {
+        meta[4 * sig + 0] = K;
+        meta[4 * sig + 1] = M;
+        meta[4 * sig + 2] = J;
+        meta[4 * sig + 3] = F > 0 ? 1 : 0;  // 0: no frame at all (pystoi raises)
+    }
+    __threadfence_block();
+    __syncthreads();
+    const int nblk = (M + FB - 1) / FB;
+    for (int b = tid; b < nblk; b += 256) {
+        int* t = btab_all + ((int64_t)sig * NBLK + b) * BT;
+        const int j0 = b * FB;
+        const int nf = min(FB, M - j0);
+        int D = 0, last = -1;
+        for (int hl = 0; hl <= nf; ++hl) {
+            const int h = j0 + hl;
+            int sb = -1;
+            if (h >= 1) {
+                const int pb = kf[h - 1] + 1;
+                if (pb != last) { t[1 + D] = pb; last = pb; ++D; }
+                sb = D - 1;
+            }
+            const int pa = kf[h];
+            if (pa != last) { t[1 + D] = pa; last = pa; ++D; }
+            t[1 + MAXD + hl] = D - 1;             // sa
+            t[1 + MAXD + (FB + 1) + hl] = sb;     // sb
+        }
+        t[0] = D;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// phase A: band envelopes of STFT frames [j0, j0 + nf) of one signal, fp64.
+// (fp32 is not enough here: STOI normalises every band separately, and an
+// fp32 FFT's roundoff, ~1e-7 of the frame's energy, is a large fraction of a
+// band that holds only a noise floor.)
+// ---------------------------------------------------------------------------
+struct __attribute__((aligned(16))) cd {
+    double x, y;
+};
+__device__ __forceinline__ cd dmk(double x, double y) { return cd{x, y}; }
+__device__ __forceinline__ cd dadd(cd a, cd b) { return cd{a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ cd dsub(cd a, cd b) { return cd{a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ cd dmul(cd a, cd b) {
+    return cd{fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x)};
+}
+
+// forward DFT4: X = [a0+a1+a2+a3, a0-i a1-a2+i a3, a0-a1+a2-a3, a0+i a1-a2-i a3]
+__device__ __forceinline__ void fdft4(cd& a0, cd& a1, cd& a2, cd& a3) {
+    const cd s02 = dadd(a0, a2), d02 = dsub(a0, a2);
+    const cd s13 = dadd(a1, a3), t = dsub(a1, a3);
+    const cd d13 = dmk(t.y, -t.x);  // -i (a1 - a3)
+    a0 = dadd(s02, s13);
+    a2 = dsub(s02, s13);
+    a1 = dadd(d02, d13);
+    a3 = dsub(d02, d13);
+}
+
+// e^{-2πi m/16}, m in [0, 9]
+__device__ __forceinline__ cd w16f(int m) {
+    constexpr double c1 = 0.92387953251128674, s1 = 0.38268343236508978, r2 = 0.70710678118654752;
+    switch (m) {
+        case 0: return dmk(1.0, 0.0);
+        case 1: return dmk(c1, -s1);
+        case 2: return dmk(r2, -r2);
+        case 3: return dmk(s1, -c1);
+        case 4: return dmk(0.0, -1.0);
+        case 5: return dmk(-s1, -c1);
+        case 6: return dmk(-r2, -r2);
+        case 7: return dmk(-c1, -s1);
+        case 8: return dmk(-1.0, 0.0);
+        default: return dmk(-c1, s1);  // 9
+    }
+}
+
+// forward DFT16 in registers (radix 4 x 4), natural order in and out
+__device__ __forceinline__ void fdft16(cd (&v)[16]) {
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) fdft4(v[k2], v[4 + k2], v[8 + k2], v[12 + k2]);
+#pragma unroll
+    for (int n1 = 1; n1 < 4; ++n1)
+#pragma unroll
+        for (int k2 = 1; k2 < 4; ++k2) {
+            const int m = n1 * k2;
+            const cd a = v[4 * n1 + k2];
+            v[4 * n1 + k2] = (m == 4) ? dmk(a.y, -a.x) : dmul(a, w16f(m));
+        }
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1) fdft4(v[4 * n1], v[4 * n1 + 1], v[4 * n1 + 2], v[4 * n1 + 3]);
+    cd t[16];
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1)
+#pragma unroll
+        for (int n2 = 0; n2 < 4; ++n2) t[n1 + 4 * n2] = v[4 * n1 + n2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = t[i];
+}
+
+struct StoiLds {
+    double wnd[stoi::FR];
+    cd tw256[256];          // e^{-2πi k/256}
+    cd tw512[256];          // e^{-2πi k/512}
+    double ola[stoi::FB + 1][stoi::HOP];
+    union {
+        struct {
+            float stage[stoi::SLOTS * stoi::SSTR];  // 16-kHz input (f32, as the cells hold it)
+            double e10[stoi::MAXD][stoi::HOP];
+        } a;
+        double t[stoi::FB][16 * 17];   // transpose, one component at a time
+        double pw[stoi::FB][224];      // |X|^2
+        struct {
+            double y[94 * 17];
+            double x[94 * 17];
+        } b;
+    } u;
+    double red[stoi::NT / 64];
+    int tab[stoi::BT];
+};
+
+// e (16 kHz) sample n of a cell: the finalize_enhanced output — y shifted by
+// the alignment lag, length-matched (zero outside [0, len)), clipped
+__device__ __forceinline__ float cell_sample(const float* y, int64_t n, int64_t len, int lag,
+                                             bool clip) {
+    const int64_t s = n - lag;
+    if (n < 0 || n >= len || s < 0 || s >= len) return 0.0f;
+    float v = y[s];
+    if (clip) v = fminf(fmaxf(v, -1.0f), 1.0f);
+    return v;
+}
+
+__device__ __forceinline__ void stoi_tables(StoiLds& L) {
+    const int tid = threadIdx.x;
+    for (int n = tid; n < stoi::FR; n += stoi::NT) L.wnd[n] = hann_m(n);
+    for (int k = tid; k < 256; k += stoi::NT) {
+        double s, c;
+        sincospi(-2.0 * k / 256.0, &s, &c);
+        L.tw256[k] = dmk(c, s);
+        sincospi(-2.0 * k / 512.0, &s, &c);
+        L.tw512[k] = dmk(c, s);
+    }
+}
+
+// PRE: the 10-kHz signal is given (clean side, fp64 x10); otherwise the 16-kHz
+// cell output is resampled here.
+template <bool PRE>
+__device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t len, int lag,
+                             bool clip, const double* __restrict__ x10,
+                             const double* __restrict__ coef, const int* __restrict__ btab,
+                             int M, double* __restrict__ env) {
+    using namespace stoi;
+    const int tid = threadIdx.x;
+    const int nblk = (M + FB - 1) / FB;
+    for (int blk = 0; blk < nblk; ++blk) {
+        const int j0 = blk * FB;
+        const int nf = min(FB, M - j0);
+        __syncthreads();  // previous block's readers of tab / union are done
+        if (tid < BT) L.tab[tid] = btab[(int64_t)blk * BT + tid];
+        __syncthreads();
+        const int D = L.tab[0];
+        // ---- 10-kHz half-blocks p = tab[1 + d] into e10[d]
+        if (PRE) {
+            for (int i = tid; i < D * HOP; i += NT) {
+                const int d = i >> 7, n = i & (HOP - 1);
+                L.u.a.e10[d][n] = x10[(int64_t)L.tab[1 + d] * HOP + n];
+            }
+        } else {
+            for (int c0 = 0; c0 < D; c0 += SLOTS) {
+                const int ns = min(SLOTS, D - c0);
+                // stage e[8 q0 - 58 + u], u < 339, at [u & 7][u >> 3]
+                for (int i = tid; i < ns * SSTR; i += NT) {
+                    const int s = i / SSTR, uu = i - s * SSTR;
+                    const int64_t p = L.tab[1 + c0 + s];
+                    const int64_t q0 = (HOP * p) / UP;
+                    const int64_t n = 8 * q0 + KLO + uu;
+                    L.u.a.stage[s * SSTR + (uu & 7) * SROW + (uu >> 3)] =
+                        uu < 8 * GRP + KN ? cell_sample(y, n, len, lag, clip) : 0.0f;
+                }
+                __syncthreads();
+                if (tid < ns * GRP) {
+                    const int s = tid / GRP, g = tid - s * GRP;
+                    const int64_t p = L.tab[1 + c0 + s];
+                    const int64_t q0 = (HOP * p) / UP;
+                    const int64_t q = q0 + g;
+                    const float* st = L.u.a.stage + s * SSTR + g;
+                    double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+                    // 16 x 8 taps (coefficients beyond the support, kk >= 123, are 0)
+#pragma unroll 1
+                    for (int kb = 0; kb < CST / 8; ++kb) {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const double e = (double)st[j * SROW + kb];
+#pragma unroll
+                            for (int r = 0; r < 5; ++r)
+                                acc[r] = fma(coef[r * CST + 8 * kb + j], e, acc[r]);
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 5; ++r) {
+                        const int64_t off = 5 * q + r - HOP * p;
+                        if (off >= 0 && off < HOP) L.u.a.e10[c0 + s][off] = acc[r];
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        __syncthreads();
+        // ---- overlap-add: ola[hl][n] = w[n] e10[sa][n] + w[128+n] e10[sb][n]
+        for (int i = tid; i < (nf + 1) * HOP; i += NT) {
+            const int hl = i >> 7, n = i & (HOP - 1);
+            const int sa = L.tab[1 + MAXD + hl];
+            const int sb = L.tab[1 + MAXD + (FB + 1) + hl];
+            double v = L.wnd[n] * L.u.a.e10[sa][n];
+            if (sb >= 0) v = fma(L.wnd[HOP + n], L.u.a.e10[sb][n], v);
+            L.ola[hl][n] = v;
+        }
+        __syncthreads();
+        // ---- 512-point rfft of frame fl = [ola[fl], ola[fl+1]] * w, 16 lanes per frame:
+        // z[m] = s[2m] + i s[2m+1] (m < 128, 0 above), Z = DFT256(z) as DFT16 x DFT16
+        {
+            const int fl = tid >> 4, n1 = tid & 15;
+            cd v[16];
+#pragma unroll
+            for (int n2 = 0; n2 < 8; ++n2) {
+                const int n = 2 * (n1 + 16 * n2);
+                const double* row = n2 < 4 ? L.ola[fl] : L.ola[fl + 1];
+                const int o = n2 < 4 ? n : n - HOP;
+                v[n2] = dmk(L.wnd[n] * row[o], L.wnd[n + 1] * row[o + 1]);
+            }
+#pragma unroll
+            for (int n2 = 8; n2 < 16; ++n2) v[n2] = dmk(0.0, 0.0);
+            fdft16(v);                                 // v[k1] = A[n1][k1]
+            {
+                const cd w = L.tw256[n1];
+                cd wr = w;
+#pragma unroll
+                for (int k1 = 1; k1 < 16; ++k1) {
+                    v[k1] = dmul(v[k1], wr);
+                    wr = dmul(wr, w);
+                }
+            }
+            double* t = L.u.t[fl];
+            const int k1 = n1;
+            double re[16];
+#pragma unroll
+            for (int a = 0; a < 16; ++a) t[a * 17 + n1] = v[a].x;
+            __syncthreads();
+#pragma unroll
+            for (int a = 0; a < 16; ++a) re[a] = t[k1 * 17 + a];
+            __syncthreads();
+#pragma unroll
+            for (int a = 0; a < 16; ++a) t[a * 17 + n1] = v[a].y;
+            __syncthreads();
+#pragma unroll
+            for (int a = 0; a < 16; ++a) v[a] = dmk(re[a], t[k1 * 17 + a]);
+            fdft16(v);                                 // v[k2] = Z[k1 + 16 k2]
+            __syncthreads();                           // t reads done before pw (aliased)
+            // partner Z[(256 - k) mod 256]: lane (16 - k1) & 15, register 15 - k2 (k1 > 0)
+            const int src = (tid & 48) | ((16 - k1) & 15);  // lane within the wave
+            double* pw = L.u.pw[fl];
+#pragma unroll
+            for (int k2 = 0; k2 < 16; ++k2) {
+                const cd zo = v[15 - k2];
+                cd zp = dmk(__shfl(zo.x, src), __shfl(zo.y, src));
+                if (k1 == 0) zp = v[(16 - k2) & 15];
+                const cd z = v[k2];
+                const cd e = dmk(0.5 * (z.x + zp.x), 0.5 * (z.y - zp.y));
+                const cd od = dmk(0.5 * (z.y + zp.y), -0.5 * (z.x - zp.x));
+                const int k = k1 + 16 * k2;
+                const cd x = dadd(e, dmul(L.tw512[k], od));  // X[k] = E + e^{-2πi k/512} O
+                if (k < 224) pw[k] = fma(x.x, x.x, x.y * x.y);
+            }
+        }
+        __syncthreads();
+        // ---- band envelopes
+        if (tid < nf * NBAND) {
+            const int fl = tid / NBAND, b = tid - fl * NBAND;
+            const double* pw = L.u.pw[fl];
+            double s = 0.0;
+            for (int k = BAND_EDGE[b]; k < BAND_EDGE[b + 1]; ++k) s += pw[k];
+            env[(int64_t)(j0 + fl) * 16 + b] = sqrt(s);
+        }
+    }
+}
+
+// clean side: envelopes, then per (segment, band) statistics
+__global__ void __launch_bounds__(stoi::NT) stoi_clean_env_kernel(const double* __restrict__ x10all,
+                                                                   int64_t n10, int64_t NBLK,
+                                                                   int64_t Mmax,
+                                                                   const int* __restrict__ meta,
+                                                                   const int* __restrict__ btab,
+                                                                   double* __restrict__ xtob) {
+    __shared__ StoiLds L;
+    const int sig = blockIdx.x;
+    stoi_tables(L);
+    const int M = meta[4 * sig + 1];
+    stoi_phase_a<true>(L, nullptr, 0, 0, false, x10all + (int64_t)sig * n10, nullptr,
+                       btab + (int64_t)sig * NBLK * stoi::BT, M, xtob + (int64_t)sig * Mmax * 16);
+}
+
+// (||x||, mean, 1/(||x - mean|| + eps)) of the clean envelope over each segment
+__global__ void __launch_bounds__(256) stoi_clean_stat_kernel(const double* __restrict__ xtob,
+                                                               int64_t Mmax, int64_t Jmax,
+                                                               const int* __restrict__ meta,
+                                                               double4* __restrict__ xstat) {
+    using namespace stoi;
+    const int sig = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int J = meta[4 * sig + 2];
+    const int j = (int)(i / 16), b = (int)(i % 16);
+    if (j >= J || b >= NBAND) return;
+    const double* x = xtob + ((int64_t)sig * Mmax + j) * 16 + b;
+    double s = 0.0, s2 = 0.0;
+    for (int t = 0; t < NSEG; ++t) {
+        const double v = x[t * 16];
+        s += v;
+        s2 = fma(v, v, s2);
+    }
+    const double mean = s / NSEG;
+    double c2 = 0.0;
+    for (int t = 0; t < NSEG; ++t) {
+        const double v = x[t * 16] - mean;
+        c2 = fma(v, v, c2);
+    }
+    xstat[((int64_t)sig * Jmax + j) * 16 + b] = make_double4(sqrt(s2), mean, 1.0 / (sqrt(c2) + EPS), 0.0);
+}
+
+// ---------------------------------------------------------------------------
+// per cell: phase A into env scratch, phase B correlations -> stoi[c]
+// ---------------------------------------------------------------------------
+struct StoiArgs {
+    const float* y;
+    const int64_t* y_offset;
+    const int32_t* lag;
+    const int32_t* sig_of;
+    int64_t len, NBLK, Mmax, Jmax;
+    int clip;
+    const double* coef;
+    const int* meta;
+    const int* btab;
+    const double* xtob;
+    const double4* xstat;
+    double* scratch;  // [n_cells][Mmax][16]
+    double* out;
+};
+
+__global__ void __launch_bounds__(stoi::NT) stoi_cells_kernel(StoiArgs a) {
+    using namespace stoi;
+    __shared__ StoiLds L;
+    const int64_t c = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int sig = a.sig_of[c];
+    const int M = a.meta[4 * sig + 1];
+    const int J = a.meta[4 * sig + 2];
+    if (a.meta[4 * sig + 3] == 0) {  // no 256-sample frame at all: pystoi raises -> None
+        if (tid == 0) a.out[c] = __builtin_nan("");
+        return;
+    }
+    if (J <= 0) {  // fewer than 30 STFT frames after silent-frame removal
+        if (tid == 0) a.out[c] = 1e-5;
+        return;
+    }
+    stoi_tables(L);
+    double* env = a.scratch + c * a.Mmax * 16;
+    const int lag = a.lag ? a.lag[c] : 0;
+    stoi_phase_a<false>(L, a.y + a.y_offset[c], a.len, lag, a.clip != 0, nullptr, a.coef,
+                        a.btab + (int64_t)sig * a.NBLK * BT, M, env);
+    __syncthreads();  // env rows of this workgroup are visible to it
+    // ---- phase B: segment j, band b
+    const double* xt = a.xtob + (int64_t)sig * a.Mmax * 16;
+    const double4* xs = a.xstat + (int64_t)sig * a.Jmax * 16;
+    constexpr double clipf = 6.623413251903491;  // 1 + 10^(-BETA/20)
+    double dsum = 0.0;
+    const int seg = tid & 63, bg = tid >> 6;
+    for (int j0 = 0; j0 < J; j0 += 64) {
+        const int rows = min(64, J - j0) + NSEG - 1;
+        __syncthreads();
+        for (int i = tid; i < rows * 16; i += NT) {
+            const int r = i >> 4, b = i & 15;
+            L.u.b.y[r * 17 + b] = env[(int64_t)(j0 + r) * 16 + b];
+            L.u.b.x[r * 17 + b] = xt[(int64_t)(j0 + r) * 16 + b];
+        }
+        __syncthreads();
+        const int j = j0 + seg;
+        if (j < J) {
+#pragma unroll 1
+            for (int b = bg; b < NBAND; b += 4) {
+                const double4 st = xs[(int64_t)j * 16 + b];
+                const double* yr = L.u.b.y + seg * 17 + b;
+                const double* xr = L.u.b.x + seg * 17 + b;
+                double yv[NSEG];
+                double ny2 = 0.0;
+#pragma unroll
+                for (int t = 0; t < NSEG; ++t) {
+                    yv[t] = yr[t * 17];
+                    ny2 = fma(yv[t], yv[t], ny2);
+                }
+                const double alpha = st.x / (sqrt(ny2) + EPS);
+                double sy = 0.0;
+#pragma unroll
+                for (int t = 0; t < NSEG; ++t) {
+                    yv[t] = fmin(yv[t] * alpha, xr[t * 17] * clipf);
+                    sy += yv[t];
+                }
+                const double my = sy / NSEG;
+                double c2 = 0.0, cr = 0.0;
+#pragma unroll
+                for (int t = 0; t < NSEG; ++t) {
+                    const double d = yv[t] - my;
+                    c2 = fma(d, d, c2);
+                    cr = fma(d, xr[t * 17] - st.y, cr);
+                }
+                dsum += (cr * st.z) / (sqrt(c2) + EPS);
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o);
+    if ((tid & 63) == 0) L.red[tid >> 6] = dsum;
+    __syncthreads();
+    if (tid == 0) {
+        double s = 0.0;
+        for (int w = 0; w < NT / 64; ++w) s += L.red[w];
+        a.out[c] = s / ((double)J * NBAND);
+    }
+}
+
+}  // namespace cse
+
+using namespace cse;
+
+extern "C" int64_t cse_stoi_workspace_bytes(int64_t n_sig, int64_t len) {
+    if (n_sig < 1 || len < 1) return -1;
+    return stoi_layout(n_sig, len).total;
+}
+
+extern "C" int64_t cse_stoi_scratch_bytes(int64_t n_cells, int64_t len) {
+    if (n_cells < 0 || len < 1) return -1;
+    return n_cells * stoi_layout(1, len).Mmax * 16 * 8;
+}
+
+extern "C" int cse_stoi_prepare(const double* clean, int64_t n_sig, int64_t len, int sr,
+                                void* workspace, cse_stream_t stream) {
+    CSE_CHECK_ARG(clean && workspace, "cse_stoi_prepare: NULL clean/workspace");
+    CSE_CHECK_ARG(sr == 16000, "cse_stoi_prepare: sr=%d (the device STOI resamples 16 kHz only)", sr);
+    CSE_CHECK_ARG(n_sig >= 1 && n_sig < 65536 && len >= 1, "cse_stoi_prepare: n_sig=%lld len=%lld",
+                  (long long)n_sig, (long long)len);
+    const StoiLayout L = stoi_layout(n_sig, len);
+    unsigned char* ws = (unsigned char*)workspace;
+    hipStream_t st = (hipStream_t)stream;
+    double* coef64 = (double*)(ws + L.coef64);
+    int* meta = (int*)(ws + L.meta);
+    double* x10 = (double*)(ws + L.x10);
+    double* en = (double*)(ws + L.en);
+    int* kf = (int*)(ws + L.kf);
+    int* btab = (int*)(ws + L.btab);
+    double* xtob = (double*)(ws + L.xtob);
+    double4* xstat = (double4*)(ws + L.xstat);
+    hipLaunchKernelGGL(stoi_coef_kernel, dim3(1), dim3(1024), 0, st, coef64);
+    const int64_t groups = (L.n10 + 4) / 5;
+    hipLaunchKernelGGL(stoi_resample_clean_kernel, dim3(ceil_div(groups, 256), (unsigned)n_sig),
+                       dim3(256), 0, st, clean, len, L.n10, (const double*)coef64, x10);
+    if (L.F > 0)
+        hipLaunchKernelGGL(stoi_energy_kernel, dim3(ceil_div(L.F, 4), (unsigned)n_sig), dim3(256), 0,
+                           st, x10, L.n10, L.F, en);
+    hipLaunchKernelGGL(stoi_select_kernel, dim3((unsigned)n_sig), dim3(256), 0, st, en, L.F, L.NBLK,
+                       meta, kf, btab);
+    if (L.Mmax > 0)
+        hipLaunchKernelGGL(stoi_clean_env_kernel, dim3((unsigned)n_sig), dim3(stoi::NT), 0, st, x10,
+                           L.n10, L.NBLK, L.Mmax, meta, btab, xtob);
+    if (L.Jmax > 0)
+        hipLaunchKernelGGL(stoi_clean_stat_kernel, dim3(ceil_div(L.Jmax * 16, 256), (unsigned)n_sig),
+                           dim3(256), 0, st, xtob, L.Mmax, L.Jmax, meta, xstat);
+    CSE_CHECK_LAUNCH("cse_stoi_prepare");
+    return CSE_OK;
+}
+
+extern "C" int cse_stoi_cells(const float* y, const int64_t* y_offset, const int32_t* lag,
+                              const int32_t* sig_of, int64_t n_cells, int64_t n_sig, int64_t len,
+                              int clip, const void* workspace, void* scratch, double* stoi_out,
+                              cse_stream_t stream) {
+    CSE_CHECK_ARG(y && y_offset && sig_of && workspace && stoi_out,
+                  "cse_stoi_cells: NULL argument");
+    CSE_CHECK_ARG(n_sig >= 1 && len >= 1, "cse_stoi_cells: n_sig=%lld len=%lld", (long long)n_sig,
+                  (long long)len);
+    if (n_cells == 0) return CSE_OK;
+    const StoiLayout L = stoi_layout(n_sig, len);
+    CSE_CHECK_ARG(L.Mmax == 0 || scratch, "cse_stoi_cells: NULL scratch");
+    const unsigned char* ws = (const unsigned char*)workspace;
+    StoiArgs a;
+    a.y = y;
+    a.y_offset = y_offset;
+    a.lag = lag;
+    a.sig_of = sig_of;
+    a.len = len;
+    a.NBLK = L.NBLK;
+    a.Mmax = L.Mmax;
+    a.Jmax = L.Jmax;
+    a.clip = clip;
+    a.coef = (const double*)(ws + L.coef64);
+    a.meta = (const int*)(ws + L.meta);
+    a.btab = (const int*)(ws + L.btab);
+    a.xtob = (const double*)(ws + L.xtob);
+    a.xstat = (const double4*)(ws + L.xstat);
+    a.scratch = (double*)scratch;
+    a.out = stoi_out;
+    hipLaunchKernelGGL(stoi_cells_kernel, dim3((unsigned)n_cells), dim3(stoi::NT), 0,
+                       (hipStream_t)stream, a);
+    CSE_CHECK_LAUNCH("cse_stoi_cells");
+    return CSE_OK;
+}

@@ -253,6 +253,35 @@ int cse_xcorr_lag(const float* head, const int64_t* head_offset, const int32_t* 
                   int32_t* lag, double* zero_energy, int32_t* status, float* corr,
                   cse_stream_t stream);
 
+/*
+ * STOI (pystoi 0.4.1 `stoi(clean, enhanced, sr, extended=False)`, the score of
+ * evaluation_metrics.py:30-36 that the reference's sweep optimises at
+ * speech_enhancement_comparison.py:180, and its noisy baseline at :115).
+ * Only sr = 16000 (the reference's target rate, :381) is supported: both
+ * signals are resampled to 10 kHz with Octave's resample filter.
+ *
+ * cse_stoi_prepare: the clean side, once per signal batch — clean [n_sig][len]
+ *   f64 -> workspace of cse_stoi_workspace_bytes(n_sig, len) bytes (10-kHz clean
+ *   in fp64, silent-frame mask, kept-frame list, clean band envelopes and
+ *   per-segment statistics).
+ * cse_stoi_cells: per cell c, the test signal e[n] = y[n - lag[c]] for
+ *   n - lag[c] in [0, len), else 0 (finalize_enhanced's shift and
+ *   length match, :61-69, :100), clipped to [-1, 1] if clip != 0 (:105),
+ *   where y = y_base + y_offset[c] is f32 [len]; clean = signal sig_of[c].
+ *   lag may be NULL (all 0).  stoi[c] = the STOI value; 1e-5 when fewer than
+ *   30 frames survive the silent-frame removal (pystoi's warning path); NaN
+ *   when the signals hold no 256-sample frame at 10 kHz (pystoi raises ->
+ *   calculate_stoi returns None).  scratch: cse_stoi_scratch_bytes(n_cells, len)
+ *   bytes of device memory (per-cell band envelopes).
+ */
+int64_t cse_stoi_workspace_bytes(int64_t n_sig, int64_t len);
+int64_t cse_stoi_scratch_bytes(int64_t n_cells, int64_t len);
+int cse_stoi_prepare(const double* clean, int64_t n_sig, int64_t len, int sr, void* workspace,
+                     cse_stream_t stream);
+int cse_stoi_cells(const float* y, const int64_t* y_offset, const int32_t* lag,
+                   const int32_t* sig_of, int64_t n_cells, int64_t n_sig, int64_t len, int clip,
+                   const void* workspace, void* scratch, double* stoi, cse_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

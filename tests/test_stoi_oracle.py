@@ -61,3 +61,11 @@ def test_identity_is_one():
     from classical_speech_enhancement_amd.synth import make_pair
     clean, _ = make_pair(3, seconds=1.5)
     assert abs(stoi_ref.stoi(clean, clean, 16000) - 1.0) < 1e-12
+
+
+def test_no_frame_is_failure():
+    """Fewer than 256 samples at 10 kHz: pystoi raises, calculate_stoi -> None."""
+    x = np.ones(300)
+    with pytest.raises(ValueError):
+        stoi_ref.stoi(x, x, 16000)
+    assert stoi_ref.calculate_stoi(x, x, 16000) is None
