@@ -11,11 +11,12 @@ The reference's batch driver writes (speech_enhancement_comparison.py):
     {stem}_{alg}_optimized_{stoi,pesq,balanced}.wav (:302-312; soundfile's
     default WAV subtype, PCM_16).
 
-pystoi / pesq are not in this image, so the STOI/PESQ fields
-are None ("NA" in the CSV) and the rows carry the one objective the engine
-scores, SNR after finalize_enhanced: the SNR-optimal cell fills the
-`*_balopt` SNR column and `best_params_snr`.  Every key of the reference row
-is present, so readers of all_results.json keep working.
+The device scores STOI (pystoi 0.4.1 restated, metrics.py) and SNR; the pesq
+extension is not in this image, so the PESQ fields are None
+("NA" in the CSV).  The STOI-optimal cell fills the `*_stoiopt` STOI/SNR
+columns and `best_params_stoi`; the SNR-optimal cell fills the `*_balopt`
+SNR column and `best_params_snr`.  Every key of the reference row is present,
+so readers of all_results.json keep working.
 """
 
 import json
@@ -39,13 +40,19 @@ SUMMARY_KEYS = (("stoi_noisy_mean", "stoi_noisy"), ("pesq_noisy_mean", "pesq_noi
                 ("snr_balopt_mean", "snr_balopt"))
 
 
-def result_row(stem, alg, sr, snr_noisy, best_snr, best_params):
-    """One all_results.json row (run_algorithm_on_pair :314-338) for an
-    SNR-scored sweep: STOI/PESQ None, SNR of the selected cell."""
+def result_row(stem, alg, sr, snr_noisy, best_snr, best_params, stoi_noisy=None,
+               stoi_best=None, stoi_params=None, snr_stoiopt=None):
+    """One all_results.json row (run_algorithm_on_pair :314-338).  STOI
+    fields come from the device STOI (the STOI-optimal cell fills
+    stoi_stoiopt / snr_stoiopt / best_params_stoi); PESQ fields are None (no
+    pesq extension), so the PESQ-opt and balance columns stay None except
+    snr_balopt, which carries the SNR-optimal cell (also snr_snropt /
+    best_params_snr)."""
     row = {k: None for k in ROW_KEYS}
     row.update(alg=alg, stem=stem, sr=int(sr), snr_noisy=snr_noisy, snr_balopt=best_snr,
-               best_params_stoi={}, best_params_pesq={}, best_params_balanced={},
-               snr_snropt=best_snr, best_params_snr=dict(best_params or {}))
+               best_params_stoi=dict(stoi_params or {}), best_params_pesq={},
+               best_params_balanced={}, snr_snropt=best_snr, best_params_snr=dict(best_params or {}),
+               stoi_noisy=stoi_noisy, stoi_stoiopt=stoi_best, snr_stoiopt=snr_stoiopt)
     return row
 
 

@@ -14,7 +14,7 @@ Here the whole (pair x algorithm x grid cell) set is one job:
                  (SURVEY §8(e)); an item larger than total/(2*world) is split
                  in cell chunks first (splitting only repeats one STFT)
   run_grid       each rank computes its cells (Engine on its GPU), then ONE
-                 all_gather of fixed-size records {cell_id, sse, snr, finite}
+                 all_gather of fixed-size records {cell_id, sse, snr, finite, stoi}
                  (RCCL over xGMI for backend "nccl", gloo in CPU tests)
   select_best    rank 0's sequential best-so-far scan in grid order
                  (speech_enhancement_comparison.py:183-216) — NOT an argmax:
@@ -22,13 +22,16 @@ Here the whole (pair x algorithm x grid cell) set is one job:
                  more than tol, so ties within tol keep the earlier cell
 
 Scores: the reference scores cells by STOI, PESQ and their balance
-(evaluation_metrics.py:30-36, 104-115); pystoi/pesq are not available in this
-image, so the device path scores by SNR of the clipped output
-(evaluation_metrics.py:39-58), the metric the reference reports next to them.
+(evaluation_metrics.py:30-36, 104-115).  The device path computes STOI
+(cse_stoi_cells, pystoi 0.4.1 restated) and the SNR of the clipped output
+(evaluation_metrics.py:39-58).  PESQ's C extension is not in this image, so
+the PESQ and balance objectives are not scored; STOI and SNR each get the
+reference's sequential selection (the reference itself skips a cell whose
+PESQ is None, :182-183 — that rule is dropped, or nothing would be selected).
 Each cell is scored like finalize_enhanced (:92-106): its output is aligned
 to the clean reference by the cross-correlation lag (on the device,
 cse_xcorr_lag), length-matched, checked for finiteness and clipped, then
-calculate_snr.
+calculate_snr and calculate_stoi.
 """
 
 import math
@@ -44,7 +47,11 @@ ALGO_WEIGHT = {"spectralSubtractor": 1.0, "wiener": 1.1, "mmse": 2.0, "omlsa": 3
 # tolerance of the best-so-far update per objective (speech_enhancement_comparison.py:183,194,205)
 TOLERANCE = {"stoi": 1e-6, "pesq": 1e-3, "balance": 1e-5, "snr": 1e-5}
 
-RECORD_FIELDS = ("cell_id", "sse", "snr", "finite")  # one float64 row per cell
+RECORD_FIELDS = ("cell_id", "sse", "snr", "finite", "stoi")  # one float64 row per cell
+TABLE_COLUMN = {"sse": 0, "snr": 1, "finite": 2, "stoi": 3}  # table = records without cell_id
+NCOL = len(RECORD_FIELDS) - 1
+# bound on the cell waveforms held at once for STOI scoring (f32 bytes)
+STOI_WAVE_BYTES = 8 << 30
 
 
 def job_specs(n_pairs, algorithms=None, grids=None, n_fft=None):
@@ -105,39 +112,58 @@ def assign_lpt(specs, lengths, world):
     return rank_of, load
 
 
-def engine_compute(clean, noisy, specs, ids, engine=None, align=True):
-    """Device compute of the cells ``ids``: per-cell (sse, snr, finite), scored
-    after finalize_enhanced's alignment (align=False: at lag 0).
+def engine_compute(clean, noisy, specs, ids, engine=None, align=True, stoi=True):
+    """Device compute of the cells ``ids``: per-cell (sse, snr, finite, stoi),
+    scored after finalize_enhanced's alignment (align=False: at lag 0).
+    stoi=False leaves the STOI column NaN (no waveforms are kept).
 
     clean/noisy: lists of 1-D float arrays (host) indexed by pair.  Pairs are
-    batched by length (the engine's signal batches are rectangular)."""
+    batched by length (the engine's signal batches are rectangular), and, when
+    STOI is scored, in groups whose cell waveforms fit STOI_WAVE_BYTES."""
     import torch
     from .engine import Engine, snr_db
+    from .metrics import StoiPlan
     eng = engine or Engine()
-    out = np.zeros((len(ids), 3))
+    out = np.full((len(ids), NCOL), np.nan)
     by_len = OrderedDict()
     for j, cid in enumerate(ids):
         pair = specs[cid][0]
-        by_len.setdefault(len(noisy[pair]), []).append(j)
-    for L, js in by_len.items():
-        pairs = sorted({specs[ids[j]][0] for j in js})
-        slot = {p: s for s, p in enumerate(pairs)}
-        nz = torch.as_tensor(np.stack([np.asarray(noisy[p], np.float64) for p in pairs])).cuda()
-        cl = torch.as_tensor(np.stack([np.asarray(clean[p], np.float64) for p in pairs])).cuda()
-        sub = [(slot[specs[ids[j]][0]], specs[ids[j]][1], specs[ids[j]][2]) for j in js]
-        res = eng.run(nz, sub, clean=cl, align=align)
-        cpow = np.array([float(np.dot(np.asarray(clean[p], np.float64),
-                                      np.asarray(clean[p], np.float64))) for p in pairs])
-        snr = snr_db(res["sse"], cpow[[s for (s, _, _) in sub]])
-        out[js, 0] = res["sse"]
-        out[js, 1] = snr
-        out[js, 2] = res["finite"]
+        by_len.setdefault(len(noisy[pair]), OrderedDict()).setdefault(pair, []).append(j)
+    for L, by_pair in by_len.items():
+        batches, cur, n_cur = [], [], 0
+        for pair, js in by_pair.items():
+            if stoi and cur and (n_cur + len(js)) * L * 4 > STOI_WAVE_BYTES:
+                batches.append(cur)
+                cur, n_cur = [], 0
+            cur.append(pair)
+            n_cur += len(js)
+        batches.append(cur)
+        for pairs in batches:
+            js = [j for p in pairs for j in by_pair[p]]
+            slot = {p: s for s, p in enumerate(pairs)}
+            nz = torch.as_tensor(np.stack([np.asarray(noisy[p], np.float64) for p in pairs])).cuda()
+            cl = torch.as_tensor(np.stack([np.asarray(clean[p], np.float64) for p in pairs])).cuda()
+            sub = [(slot[specs[ids[j]][0]], specs[ids[j]][1], specs[ids[j]][2]) for j in js]
+            res = eng.run(nz, sub, clean=cl, align=align, want_waveforms=stoi)
+            cpow = np.array([float(np.dot(np.asarray(clean[p], np.float64),
+                                          np.asarray(clean[p], np.float64))) for p in pairs])
+            sig = np.array([s for (s, _, _) in sub], dtype=np.int64)
+            out[js, 0] = res["sse"]
+            out[js, 1] = snr_db(res["sse"], cpow[sig])
+            out[js, 2] = res["finite"]
+            if stoi:
+                lag = res["lag"] if align else np.zeros(len(sub), dtype=np.int64)
+                plan = StoiPlan(cl)
+                sc = plan.score(res["y"].view(-1), np.arange(len(sub), dtype=np.int64) * L, sig,
+                                lag=lag, clip=True)
+                out[js, 3] = np.where(res["finite"], sc, np.nan)
+                del plan, res
     return out
 
 
 def gather_records(local, n_total, group=None, device=None):
-    """All-gather per-cell records [n_local, 4] (cell_id, sse, snr, finite)
-    from every rank into one [n_total, 3] table indexed by cell_id.  Fixed-size
+    """All-gather per-cell records [n_local, 1 + NCOL] (RECORD_FIELDS) from
+    every rank into one [n_total, NCOL] table indexed by cell_id.  Fixed-size
     rows padded to the largest shard so one all_gather_into_tensor moves them."""
     import torch
     import torch.distributed as dist
@@ -145,21 +171,22 @@ def gather_records(local, n_total, group=None, device=None):
         world = 1
     else:
         world = dist.get_world_size(group)
-    rec = torch.as_tensor(np.asarray(local, dtype=np.float64).reshape(-1, 4))
+    width = 1 + NCOL
+    rec = torch.as_tensor(np.asarray(local, dtype=np.float64).reshape(-1, width))
     if world > 1:
         n = torch.tensor([rec.shape[0]], dtype=torch.int64, device=device)
         counts = torch.zeros(world, dtype=torch.int64, device=device)
         dist.all_gather_into_tensor(counts, n, group=group)
         m = int(counts.max())
-        pad = torch.full((m, 4), -1.0, dtype=torch.float64)
+        pad = torch.full((m, width), -1.0, dtype=torch.float64)
         pad[:rec.shape[0]] = rec
         pad = pad.to(device) if device is not None else pad
-        allrec = torch.empty((world * m, 4), dtype=torch.float64, device=pad.device)
+        allrec = torch.empty((world * m, width), dtype=torch.float64, device=pad.device)
         dist.all_gather_into_tensor(allrec, pad, group=group)
         rec = allrec.cpu()
     rec = rec.numpy()
     rec = rec[rec[:, 0] >= 0]
-    table = np.full((n_total, 3), np.nan)
+    table = np.full((n_total, NCOL), np.nan)
     ids = rec[:, 0].astype(np.int64)
     if len(np.unique(ids)) != len(ids) or len(ids) != n_total:
         raise RuntimeError(f"gather: {len(ids)} records for {n_total} cells "
@@ -173,9 +200,12 @@ def select_best(specs, table, objective="snr", tol=None):
 
     Non-finite cells are skipped like finalize_enhanced returning None
     (speech_enhancement_comparison.py:102-103,173-175); the incumbent starts
-    at -1 (:126-141).  Returns {(pair, alg): (cell_id or -1, score)}."""
+    at -1 (:126-141); a NaN score (pystoi failure -> None) is skipped like
+    :182-183.  Returns {(pair, alg): (cell_id or -1, score)}."""
     tol = TOLERANCE[objective] if tol is None else tol
-    col = {"snr": 1}[objective]
+    if objective not in ("snr", "stoi"):
+        raise ValueError(f"objective {objective!r} is not scored on the device (pesq is absent)")
+    col = TABLE_COLUMN[objective]
     groups = OrderedDict()
     for cid, (pair, alg, _) in enumerate(specs):
         groups.setdefault((pair, alg), []).append(cid)
@@ -186,6 +216,8 @@ def select_best(specs, table, objective="snr", tol=None):
             if not table[cid, 2]:
                 continue
             s = table[cid, col]
+            if s != s:  # NaN
+                continue
             if s > incumbent + tol:
                 incumbent, win = s, cid
         best[key] = (win, incumbent if win >= 0 else None)
@@ -194,7 +226,7 @@ def select_best(specs, table, objective="snr", tol=None):
 
 def run_grid(clean, noisy, specs, compute=None, group=None, device=None, objective="snr"):
     """Run every cell of ``specs`` across the ranks of ``group`` (or locally)
-    and return (table [n_cells, 3] = sse, snr, finite, winners).  Every rank
+    and return (table [n_cells, NCOL] = sse, snr, finite, stoi, winners).  Every rank
     gets the full table (all_gather); the selection is the deterministic
     sequential scan, identical on every rank."""
     import torch.distributed as dist
@@ -205,19 +237,36 @@ def run_grid(clean, noisy, specs, compute=None, group=None, device=None, objecti
     rank_of, _ = assign_lpt(specs, lengths, world)
     ids = np.nonzero(rank_of == rank)[0]
     compute = compute or engine_compute
-    vals = compute(clean, noisy, specs, ids) if len(ids) else np.zeros((0, 3))
+    vals = compute(clean, noisy, specs, ids) if len(ids) else np.zeros((0, NCOL))
     local = np.concatenate([ids[:, None].astype(np.float64), vals], axis=1)
     table = gather_records(local, len(specs), group=group, device=device)
     return table, select_best(specs, table, objective)
 
 
+def _snr_baseline(c, n):
+    m = min(len(c), len(n))
+    err = np.sum((c[:m] - n[:m]) ** 2)
+    return math.inf if err == 0 else float(10 * np.log10(np.sum(c[:m] ** 2) / (err + 1e-10)))
+
+
+def _device_stoi(clean, test, sr):
+    from .metrics import calculate_stoi
+    return calculate_stoi(clean, test, sr)
+
+
+def _opt(v):
+    return None if v != v else float(v)
+
+
 def optimize_parameters(clean_reference, noisy_audio, sr, algorithm, param_ranges=None,
-                        compute=None):
+                        compute=None, stoi_fn=None):
     """Single-pair, single-algorithm mirror of the reference's
-    optimize_parameters (speech_enhancement_comparison.py:108-263) scored by
-    SNR: returns {'snr': {'score', 'params', 'cell'}, 'baseline': {'snr'},
-    'improvements': {'snr'}}; raises ValueError like :251-253 when no cell
-    produced a finite output."""
+    optimize_parameters (speech_enhancement_comparison.py:108-263), scored by
+    STOI and SNR: returns {'stoi': {'score', 'params', 'cell', 'snr'},
+    'snr': {'score', 'params', 'cell', 'stoi'}, 'baseline': {'stoi', 'snr'},
+    'improvements': {'stoi', 'snr'}, 'table'}; raises ValueError like :251-253
+    when no cell produced a finite output.  The 'stoi' entry is None when no
+    cell has a STOI value (a compute function that does not score STOI)."""
     from .engine import canonical_algo
     if sr != 16000:
         raise ValueError("the device path runs at 16 kHz (prepare_pair resamples to 16 kHz)")
@@ -230,26 +279,35 @@ def optimize_parameters(clean_reference, noisy_audio, sr, algorithm, param_range
     cid, score = best[(0, alg)]
     if cid < 0:
         raise ValueError("Optimization failed for snr - no valid parameters found!")
-    c, n = clean[0], noisy[0]
-    m = min(len(c), len(n))
-    err = np.sum((c[:m] - n[:m]) ** 2)
-    base = math.inf if err == 0 else float(10 * np.log10(np.sum(c[:m] ** 2) / (err + 1e-10)))
-    return {"snr": {"score": score, "params": dict(specs[cid][2]), "cell": int(cid)},
-            "baseline": {"snr": base}, "improvements": {"snr": score - base},
-            "table": table}
+    base = _snr_baseline(clean[0], noisy[0])
+    out = {"snr": {"score": score, "params": dict(specs[cid][2]), "cell": int(cid),
+                   "stoi": _opt(table[cid, 3])},
+           "baseline": {"snr": base}, "improvements": {"snr": score - base}, "table": table,
+           "stoi": None}
+    sid, sscore = select_best(specs, table, "stoi")[(0, alg)]
+    if sid >= 0:
+        bstoi = (stoi_fn or _device_stoi)(clean[0], noisy[0], sr) or 0  # :115 "or 0"
+        out["stoi"] = {"score": sscore, "params": dict(specs[sid][2]), "cell": int(sid),
+                       "snr": float(table[sid, 1])}
+        out["baseline"]["stoi"] = bstoi
+        out["improvements"]["stoi"] = sscore - bstoi
+    return out
 
 
 def run_sweep(clean, noisy, stems, out_root, sr=16000, algorithms=None, grids=None,
               group=None, device=None):
     """The reference's batch driver (main, speech_enhancement_comparison.py:378-474)
     on the device: every pair x algorithm x grid cell scored after
-    finalize_enhanced, the SNR-best cell per (pair, algorithm) selected by the
-    sequential tolerance scan, its waveform written as
-    results_{alg}/{stem}_{alg}_optimized_snr.wav, and the summary files
+    finalize_enhanced (STOI and SNR), the STOI-best and SNR-best cells per
+    (pair, algorithm) selected by the sequential tolerance scan, their
+    waveforms written as results_{alg}/{stem}_{alg}_optimized_stoi.wav (the
+    reference's name, :303) and ..._optimized_snr.wav, and the summary files
     (results.write_summary) under results_summary/.  Rank 0 writes."""
+    import torch
     import torch.distributed as dist
     from . import results
     from .engine import Engine
+    from .metrics import StoiPlan
     grids = grids or ALGORITHM_GRIDS
     algorithms = list(algorithms or grids)
     specs = job_specs(len(noisy), algorithms, grids)
@@ -257,28 +315,38 @@ def run_sweep(clean, noisy, stems, out_root, sr=16000, algorithms=None, grids=No
     rank = dist.get_rank(group) if (dist.is_available() and dist.is_initialized()) else 0
     if rank != 0:
         return None
+    best_stoi = select_best(specs, table, "stoi")
     eng = Engine()
     rows = []
     for pair, stem in enumerate(stems):
         c = np.asarray(clean[pair], np.float64)
         n = np.asarray(noisy[pair], np.float64)
+        snr_noisy = _snr_baseline(c, n)
         m = min(len(c), len(n))
-        err = np.sum((c[:m] - n[:m]) ** 2)
-        snr_noisy = math.inf if err == 0 else float(10 * np.log10(np.sum(c[:m] ** 2) / (err + 1e-10)))
+        plan = StoiPlan(torch.as_tensor(c[:m]).cuda().view(1, -1))
+        nf = torch.as_tensor(n[:m].astype(np.float32)).cuda()
+        stoi_noisy = _opt(plan.score(nf, [0], [0], clip=False)[0])
+        x = torch.as_tensor(n).cuda().view(1, -1)
+        cl = torch.as_tensor(c).cuda().view(1, -1)
         for alg in algorithms:
             cid, score = best[(pair, alg)]
             if cid < 0:
                 raise ValueError(f"Optimization failed for snr - no valid parameters found! ({stem}, {alg})")
-            params = specs[cid][2]
-            import torch
-            x = torch.as_tensor(n).cuda().view(1, -1)
-            cl = torch.as_tensor(c).cuda().view(1, -1)
-            res = eng.run(x, [(0, alg, params)], clean=cl, want_waveforms=True, align=True)
-            y = res["y"][0].cpu().numpy().astype(np.float64)
-            e = results.shift_and_fit(y, int(res["lag"][0]), len(c))
+            sid, sscore = best_stoi[(pair, alg)]
             out_dir = os.path.join(out_root, f"results_{alg}")
             os.makedirs(out_dir, exist_ok=True)
-            results.write_wav_pcm16(os.path.join(out_dir, f"{stem}_{alg}_optimized_snr.wav"), e, sr)
-            rows.append(results.result_row(stem, alg, sr, snr_noisy, float(score), params))
+            for tag, k in (("snr", cid), ("stoi", sid)):
+                if k < 0:
+                    continue
+                res = eng.run(x, [(0, alg, specs[k][2])], clean=cl, want_waveforms=True, align=True)
+                y = res["y"][0].cpu().numpy().astype(np.float64)
+                e = results.shift_and_fit(y, int(res["lag"][0]), len(c))
+                results.write_wav_pcm16(os.path.join(out_dir, f"{stem}_{alg}_optimized_{tag}.wav"),
+                                        e, sr)
+            rows.append(results.result_row(
+                stem, alg, sr, snr_noisy, float(score), specs[cid][2], stoi_noisy=stoi_noisy,
+                stoi_best=None if sid < 0 else float(sscore),
+                stoi_params=None if sid < 0 else specs[sid][2],
+                snr_stoiopt=None if sid < 0 else float(table[sid, 1])))
     results.write_summary(rows, algorithms, os.path.join(out_root, "results_summary"))
     return rows

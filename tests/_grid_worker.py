@@ -27,13 +27,16 @@ def pairs(n=3, seconds=0.3):
     return [c for c, _ in out], [x for _, x in out]
 
 
-def oracle_compute(clean, noisy, specs, ids, align=True):
-    """Per-cell (sse, snr, finite) from the CPU oracle: finalize_enhanced
-    (alignment, length match, finiteness, clip) then calculate_snr, like the
-    reference's grid loop (speech_enhancement_comparison.py:165-180); align=False
-    scores the clipped output at lag 0."""
+def oracle_compute(clean, noisy, specs, ids, align=True, stoi=True):
+    """Per-cell (sse, snr, finite, stoi) from the CPU oracle: finalize_enhanced
+    (alignment, length match, finiteness, clip) then calculate_snr and
+    calculate_stoi, like the reference's grid loop
+    (speech_enhancement_comparison.py:165-180); align=False scores the clipped
+    output at lag 0; stoi=False leaves the STOI column NaN.  STOI sees the
+    output rounded to f32, the type the device writes."""
     import oracle
-    out = np.zeros((len(ids), 3))
+    from oracle import stoi_ref
+    out = np.zeros((len(ids), 4))
     for j, cid in enumerate(ids):
         pair, alg, p = specs[cid]
         kw = dict(p)
@@ -43,9 +46,14 @@ def oracle_compute(clean, noisy, specs, ids, align=True):
         c = np.asarray(clean[pair], np.float64)
         e = oracle.finalize_enhanced(y, c, 16000, do_align=align)
         if e is None:
-            out[j] = (np.nan, np.nan, 0)
+            out[j] = (np.nan, np.nan, 0, np.nan)
             continue
-        out[j] = (np.sum((c - e) ** 2), oracle.calculate_snr(c, e), 1)
+        st = None
+        if stoi:
+            e32 = oracle.finalize_enhanced(np.asarray(y, np.float32).astype(np.float64), c, 16000,
+                                           do_align=align)
+            st = stoi_ref.calculate_stoi(c, e32, 16000)
+        out[j] = (np.sum((c - e) ** 2), oracle.calculate_snr(c, e), 1, np.nan if st is None else st)
     return out
 
 

@@ -18,7 +18,7 @@ def test_run_sweep_files_and_selection(tmp_path):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    clean, noisy = pairs(2, 0.6)
+    clean, noisy = pairs(2, 1.2)
     stems = ["p00", "p01"]
     grids = {k: SMALL_GRIDS[k] for k in ("spectralSubtractor", "mmse")}
     rows = search.run_sweep(clean, noisy, stems, str(tmp_path), grids=grids)
@@ -26,11 +26,19 @@ def test_run_sweep_files_and_selection(tmp_path):
     specs = search.job_specs(2, list(grids), grids)
     ref = oracle_compute(clean, noisy, specs, np.arange(len(specs)))
     best = search.select_best(specs, ref)
+    best_stoi = search.select_best(specs, ref, "stoi")
+    from oracle import stoi_ref
     for r in rows:
         pair = stems.index(r["stem"])
         cid, score = best[(pair, r["alg"])]
         # the device pick scores within float noise of the oracle's pick
         assert abs(r["snr_balopt"] - score) < 1e-3, r
+        sid, sscore = best_stoi[(pair, r["alg"])]
+        assert abs(r["stoi_stoiopt"] - sscore) < 4e-6, r
+        assert abs(r["stoi_noisy"] - stoi_ref.stoi(clean[pair], noisy[pair].astype(np.float32)
+                                                   .astype(np.float64), 16000)) < 1e-8
+        assert os.path.exists(os.path.join(tmp_path, f"results_{r['alg']}",
+                                           f"{r['stem']}_{r['alg']}_optimized_stoi.wav"))
         path = os.path.join(tmp_path, f"results_{r['alg']}", f"{r['stem']}_{r['alg']}_optimized_snr.wav")
         y, sr = results.read_wav_pcm16(path)
         assert sr == 16000 and len(y) == len(clean[pair])

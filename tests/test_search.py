@@ -55,7 +55,7 @@ def _groups(specs):
 def test_select_best_is_the_sequential_scan():
     rng = np.random.default_rng(3)
     specs = search.job_specs(2, grids=SMALL_GRIDS)
-    table = np.zeros((len(specs), 3))
+    table = np.zeros((len(specs), 4))
     # scores with near-ties inside the tolerance, and some skipped cells
     table[:, 1] = np.round(rng.normal(5, 0.01, len(specs)), 5) + rng.choice([0, 4e-6], len(specs))
     table[:, 2] = rng.random(len(specs)) > 0.1
@@ -107,8 +107,9 @@ def test_run_grid_world2_gloo_matches_single_process(tmp_path):
 def test_optimize_parameters_mirror():
     clean, noisy = pairs(1, 0.25)
     grid = SMALL_GRIDS["spectralSubtractor"]
+    from oracle import stoi_ref
     res = search.optimize_parameters(clean[0], noisy[0], 16000, "spectralSubtractor", grid,
-                                     compute=oracle_compute)
+                                     compute=oracle_compute, stoi_fn=stoi_ref.calculate_stoi)
     cells = oracle.grid_cells(grid)
     scores = []
     for p in cells:
@@ -119,6 +120,9 @@ def test_optimize_parameters_mirror():
     assert res["snr"]["params"] == cells[w]
     assert res["snr"]["score"] == scores[w]
     assert res["baseline"]["snr"] == pytest.approx(oracle.calculate_snr(clean[0], noisy[0]))
+    # 0.25-s clips hold < 30 STOI frames: every cell scores 1e-5, the first wins
+    assert res["stoi"]["score"] == 1e-5 and res["stoi"]["params"] == cells[0]
+    assert res["baseline"]["stoi"] == 1e-5
     with pytest.raises(ValueError):
         search.optimize_parameters(clean[0], noisy[0], 8000, "spectralSubtractor", grid,
                                    compute=oracle_compute)
