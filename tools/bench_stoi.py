@@ -1,0 +1,65 @@
+"""Throughput of the device STOI (cse_stoi_cells) on 10-s cells (GPU box).
+
+    python tools/bench_stoi.py [--cells N --pairs P --reps R]
+
+Cells are noisy versions of P synthetic 10-s clean signals (random gains and
+lags, some outputs beyond [-1, 1] so the clip path runs).  Prints one JSON
+line: cells/s, ms per launch, and the per-cell fp64 work estimate.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from classical_speech_enhancement_amd.metrics import StoiPlan  # noqa: E402
+from classical_speech_enhancement_amd.synth import make_pair  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cells", type=int, default=4096)
+    ap.add_argument("--pairs", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--seconds", type=float, default=10.0)
+    a = ap.parse_args()
+    pairs = [make_pair(100 + i, a.seconds) for i in range(a.pairs)]
+    clean = torch.as_tensor(np.stack([c for c, _ in pairs])).cuda()
+    L = clean.shape[1]
+    rng = np.random.default_rng(0)
+    noisy = torch.as_tensor(np.stack([n for _, n in pairs]).astype(np.float32)).cuda()
+    sig = np.arange(a.cells) % a.pairs
+    gains = torch.as_tensor(rng.uniform(0.3, 3.0, a.cells).astype(np.float32)).cuda()
+    y = (noisy[torch.as_tensor(sig).cuda()] * gains[:, None]).contiguous().view(-1)
+    lag = rng.integers(-1600, 1601, a.cells)
+    t0 = time.perf_counter()
+    plan = StoiPlan(clean)
+    torch.cuda.synchronize()
+    prep_ms = (time.perf_counter() - t0) * 1e3
+    off = np.arange(a.cells, dtype=np.int64) * L
+    plan.score_async(y, off, sig, lag=lag)  # warm-up (scratch allocation)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(a.reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = plan.score_async(y, off, sig, lag=lag)
+        e1.record()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1))
+    ms = float(np.median(times))
+    v = out.cpu().numpy()
+    assert np.isfinite(v).all()
+    print(json.dumps({"what": "cse_stoi_cells", "cells": a.cells, "clip_s": a.seconds,
+                      "ms_per_launch": ms, "cells_per_s": a.cells / (ms / 1e3),
+                      "prepare_ms_incl_first_launch": prep_ms, "stoi_mean": float(v.mean())}))
+
+
+if __name__ == "__main__":
+    main()
