@@ -245,6 +245,11 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 #define CSE_PREFETCH_AT 0
 #endif
 
+// CSE_LDS_PAD: extra LDS bytes per workgroup (occupancy experiments only)
+#ifndef CSE_LDS_PAD
+#define CSE_LDS_PAD 0
+#endif
+
 template <int NFFT>
 struct WG {
     using G = Geo<NFFT>;
@@ -276,14 +281,14 @@ struct WG {
     // (512/256), whose wss is not constant; row stride 20 floats (disjoint banks)
     static constexpr int ISTR = 20;
     static constexpr int OFF_IWS = OFF_WIN + G::L * WSTR * 4;
-    static constexpr int BYTES = OFF_IWS + (NFFT == 512 ? G::L * ISTR * 4 : 0);
+    static constexpr int BYTES = OFF_IWS + (NFFT == 512 ? G::L * ISTR * 4 : 0) + CSE_LDS_PAD;
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
 // LDS decides how many workgroups share a CU: keep >= 12 waves (3 per SIMD)
-static_assert((163840 / WG<512>::BYTES) * CSE_WG_WAVES >= 12,
+static_assert(CSE_LDS_PAD || (163840 / WG<512>::BYTES) * CSE_WG_WAVES >= 12,
               "n_fft=512 workgroups must fill 12 waves per CU");
-static_assert((163840 / WG<1024>::BYTES) * CSE_WG_WAVES >= 8,
+static_assert(CSE_LDS_PAD || (163840 / WG<1024>::BYTES) * CSE_WG_WAVES >= 8,
               "n_fft=1024 workgroups must fill 8 waves per CU");
 static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
               WG<1024>::CPWG == CSE_CELLS_PER_GROUP(1024), "cse.h slot-group size");
@@ -540,7 +545,9 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     // ---- row staging: thread tid owns Y/N elements tid + u*THREADS, clean tid + u*THREADS
     float2 py[W::YPT];
     float pn[W::YPT];
-    float pc[W::CPT];
+    // clean samples stay f64 in flight: converting at load time made the
+    // compiler wait (vmcnt(0)) for every row load right after issuing them
+    double pc[W::CPT];
     auto load_rows = [&](int t) {  // issue loads of frame t's rows into registers
         if (t < nf) {
 #pragma unroll
@@ -556,7 +563,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         for (int u = 0; u < W::CPT; ++u) {
             const int j = tid + u * W::THREADS;
             const int o = t * HOP - NFFT / 2 + j + lag;  // clean sample scored against y[o - lag]
-            pc[u] = (j < HOP && cbase && o >= 0 && o < len) ? (float)cbase[o] : 0.0f;
+            pc[u] = (j < HOP && cbase && o >= 0 && o < len) ? cbase[o] : 0.0;
         }
     };
     // rows of frame t live in buffer t&1 (static noise: written to both once)
@@ -722,13 +729,9 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             }
             if (!(CSE_ABLATE & 2)) idft16(v);
             CSE_MARK("window");
-            // ---------------- synthesis window (/n_fft) --------------------
-            {
-                const float* wt = (const float*)__builtin_assume_aligned(
-                    smem + opaque(W::OFF_WIN + 4 * W::WSTR * i), 16);
+            // the synthesis window (/n_fft) is applied by the overlap-add FMAs below
 #pragma unroll
-                for (int q = 0; q < 32; ++q) x[q] = ((q & 1) ? v[q >> 1].y : v[q >> 1].x) * wt[q];
-            }
+            for (int q = 0; q < 32; ++q) x[q] = (q & 1) ? v[q >> 1].y : v[q >> 1].x;
         } else {
 #if !CSE_DIRECT_ROWS
             __syncthreads();  // flush frames: clean row t visible, row t-1 reads done
@@ -750,11 +753,18 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         // sum of the clipped sample (evaluation_metrics.py:52-56).  Steady
         // frames use the closed-form wss; the first R-1 and the flush frames
         // sum the covering windows explicitly.
+        // windowed overlap-add: x * w(n)/n_fft folded into the accumulating FMAs
+        // (x = 0 in flush frames, so they leave the sums unchanged)
         float done[F];
+        {
+            const float* wt = (const float*)__builtin_assume_aligned(
+                smem + opaque(W::OFF_WIN + 4 * W::WSTR * i), 16);
 #pragma unroll
-        for (int q = 0; q < F; ++q) done[q] = acc[q] + x[q];
+            for (int q = 0; q < F; ++q) done[q] = fmaf(x[q], wt[q], acc[q]);
 #pragma unroll
-        for (int q = 0; q < PEND; ++q) acc[q] = (q + F < PEND ? acc[q + F] : 0.0f) + x[q + F];
+            for (int q = 0; q < PEND; ++q)
+                acc[q] = fmaf(x[q + F], wt[q + F], q + F < PEND ? acc[q + F] : 0.0f);
+        }
         if (valid && !(CSE_ABLATE & 4)) {
             const int o0 = t * HOP + off - NFFT / 2;  // output index of q = 0
 #if CSE_DIRECT_ROWS
