@@ -1,0 +1,86 @@
+"""The multi-rank paths on one GPU (needs a GPU): two ranks share the card and
+talk over gloo, the way the 8-GPU node runs them over RCCL (one process per
+GPU).  Checks that bench.py's weak-scaling line counts both ranks' work and
+that the sharded device sweep (search.run_grid) gives every rank the same
+table as one process computing every cell."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    # device_count() does not initialise the GPU in this process (is_available()
+    # would): the ranks below are started as child processes, which must not
+    # be forked from a process that holds GPU state
+    import torch
+    if torch.cuda.device_count() == 0:
+        pytest.skip("no GPU")
+
+
+def test_bench_two_ranks_weak_scaling(gpu):
+    env = dict(os.environ, CSE_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--pairs", "1", "--seconds", "2", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 prints the one line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    units = d["config"]["units_per_step_per_gpu"]
+    assert d["value"] == pytest.approx(2 * units * d["steps"] / (d["ms_per_step"] * d["steps"] / 1e3),
+                                       rel=1e-6)
+
+
+def _rank(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from classical_speech_enhancement_amd import search
+    from _grid_worker import SMALL_GRIDS, pairs
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        clean, noisy = pairs(3, 1.2)
+        specs = search.job_specs(len(noisy), grids=SMALL_GRIDS)
+        table, best = search.run_grid(clean, noisy, specs)
+        np.save(os.path.join(outdir, f"rank{rank}.npy"), table)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_run_grid_two_ranks_equals_one_process(gpu, tmp_path):
+    import torch.multiprocessing as tmp
+    from classical_speech_enhancement_amd import search
+    from _grid_worker import SMALL_GRIDS, pairs
+    tmp.spawn(_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    # the reference table: this process touches the GPU only after the ranks exited
+    t0 = np.load(tmp_path / "rank0.npy")
+    t1 = np.load(tmp_path / "rank1.npy")
+    clean, noisy = pairs(3, 1.2)
+    specs = search.job_specs(len(noisy), grids=SMALL_GRIDS)
+    ref, _ = search.run_grid(clean, noisy, specs)
+    assert np.array_equal(t0, t1, equal_nan=True)
+    assert np.array_equal(t0, ref, equal_nan=True)
