@@ -210,10 +210,18 @@ class GridPlan:
         # ---- noise keys -> pool slices.  Each key = a base estimate (method,
         # pct, eps) post-processed by one cse_noise_finish job (smoothing,
         # fix_length zero-padding, 1/max(.,eps)); base estimates are shared.
-        keys = {}
+        # noise key of every item, computed once per distinct
+        # (algorithm, hop, method, percentile, noise_mu)
+        keys, key_cache = {}, {}
+        item_key = []
         for (_, _, alg, p) in items:
-            T = n_frames(L, p["hop_length"])
-            keys.setdefault((p["hop_length"], noise_key(alg, p, T)), None)
+            hop = p["hop_length"]
+            ck = (alg, hop, p["noise_method"], p.get("noise_percentile"), p.get("noise_mu"))
+            k = key_cache.get(ck)
+            if k is None:
+                k = key_cache[ck] = (hop, noise_key(alg, p, n_frames(L, hop)))
+                keys.setdefault(k, None)
+            item_key.append(k)
         self.keys = list(keys)
         self.pool_off, noff = {}, 0
         self.raw_off, roff = {}, 0
@@ -248,28 +256,35 @@ class GridPlan:
         Tmax = max(n_frames(L, h) for h in self.hops)
         self.ws = torch.empty(int(eng.lib.cse_noise_workspace_bytes(S, Tmax, B)),
                               dtype=torch.uint8, device=dev)
-        # ---- cell table
-        cells = np.zeros(len(items), dtype=_lib.CELL_DTYPE)
-        g_total = 0
-        self.g_offsets = []
-        for c, (idx, sig, alg, p) in enumerate(items):
-            code, _, names = ALGOS[alg]
-            hop = p["hop_length"]
-            T = n_frames(L, hop)
-            o, stride, per_sig = self.pool_off[(hop, noise_key(alg, p, T))]
-            cells["algo"][c] = _lib.ALGO[code]
-            cells["hop"][c] = hop
-            cells["y_offset"][c] = self.y_base[hop] + sig * T * B
-            cells["noise_offset"][c] = o + sig * per_sig
-            cells["noise_stride"][c] = stride
-            cells["clean_offset"][c] = sig * L if with_clean else -1
-            cells["out_offset"][c] = idx * L if want_y else -1
-            cells["gain_offset"][c] = g_total if want_g else -1
-            self.g_offsets.append((g_total, T))
-            if want_g:
-                g_total += T * B
-            prm = [float(p[k]) for k in names]
-            cells["param"][c, :len(prm)] = prm
+        # ---- cell table (columns gathered once, written as arrays)
+        n = len(items)
+        cells = np.zeros(n, dtype=_lib.CELL_DTYPE)
+        self.idx = np.fromiter((it[0] for it in items), dtype=np.int64, count=n)
+        sig = np.fromiter((it[1] for it in items), dtype=np.int64, count=n)
+        hop = np.fromiter((it[3]["hop_length"] for it in items), dtype=np.int64, count=n)
+        algo = np.fromiter((_lib.ALGO[ALGOS[it[2]][0]] for it in items), dtype=np.int32, count=n)
+        kinfo = np.array([self.pool_off[k] for k in item_key], dtype=np.int64).reshape(n, 3)
+        T = 1 + L // hop
+        ybase = np.zeros(n, dtype=np.int64)
+        for h in self.hops:
+            ybase[hop == h] = self.y_base[h]
+        cells["algo"] = algo
+        cells["hop"] = hop
+        cells["y_offset"] = ybase + sig * T * B
+        cells["noise_offset"] = kinfo[:, 0] + sig * kinfo[:, 2]
+        cells["noise_stride"] = kinfo[:, 1]
+        cells["clean_offset"] = sig * L if with_clean else -1
+        cells["out_offset"] = self.idx * L if want_y else -1
+        goff = (np.concatenate([[0], np.cumsum(T * B)[:-1]]) if want_g
+                else np.zeros(n, dtype=np.int64))
+        cells["gain_offset"] = goff if want_g else -1
+        self.g_offsets = list(zip(goff.tolist(), T.tolist()))
+        g_total = int((T * B).sum()) if want_g else 0
+        prm = np.zeros((n, 8), dtype=np.float32)
+        for c, (_, _, alg, p) in enumerate(items):
+            names = ALGOS[alg][2]
+            prm[c, :len(names)] = [p[k] for k in names]
+        cells["param"] = prm
         self.cells = cells
         packed, self.order = pack_waves(cells, n_fft)
         self.n_packed = len(packed)
@@ -281,7 +296,7 @@ class GridPlan:
         self.clean = None
         self.with_clean = with_clean
         # frame-gain evaluations (SURVEY §8(d) unit): sum over cells of frames
-        self.units = int(sum(n_frames(L, p["hop_length"]) for (_, _, _, p) in items))
+        self.units = int(T.sum())
         # ---- finalize_enhanced alignment (speech_enhancement_comparison.py:38-69)
         self.rerun = None
         self.xc_n = min(L, ALIGN_CORR_SAMPLES)
@@ -298,8 +313,7 @@ class GridPlan:
                 packed, _ = pack_waves(self.cells, n_fft)
                 self.cells_d = torch.from_numpy(packed.view(np.uint8).copy()).to(dev)
             self.head_off = torch.as_tensor(head_off, device=dev)
-            self.sig_of = torch.as_tensor(np.array([sig for (_, sig, _, _) in items],
-                                                   dtype=np.int32), device=dev)
+            self.sig_of = torch.as_tensor(sig.astype(np.int32), device=dev)
             self.xc_ws = torch.empty(int(eng.lib.cse_xcorr_workspace_bytes(
                 S, L, self.xc_n, self.xc_lag_max)), dtype=torch.uint8, device=dev)
             self.lag_d = torch.zeros(len(items), dtype=torch.int32, device=dev)
@@ -440,19 +454,28 @@ class MultiPlan:
         self.y_all = (torch.zeros((self.n, L), dtype=torch.float32, device=eng.device)
                       if want_y else None)
         by_fft = {}
+        checked = set()
         for idx, (sig, alg, params) in enumerate(specs):
             alg = canonical_algo(alg)
-            p = dict(DEFAULTS.get(alg, {}))
-            p.update(params)
-            if p["hop_length"] not in (128, 256) or p["n_fft"] not in (512, 1024):
-                raise ValueError("engine supports n_fft in {512,1024}, hop in {128,256}")
+            d = DEFAULTS.get(alg)
+            if d:
+                p = dict(d)
+                p.update(params)
+            else:
+                p = params
+            hop, nf = p["hop_length"], p["n_fft"]
             if not 0 <= int(sig) < S:
                 raise ValueError(f"signal index {sig} out of range")
-            noise_key(alg, p, n_frames(L, p["hop_length"]))  # validates the method
-            if (p["noise_method"] == "true_noise" and not with_clean
-                    and n_frames(L, p["hop_length"]) >= 5):
-                raise ValueError("TrueNoiseEstimator requires clean_audio and noisy_audio")
-            by_fft.setdefault(int(p["n_fft"]), []).append((idx, int(sig), alg, p))
+            ck = (alg, hop, nf, p["noise_method"])
+            if ck not in checked:  # per distinct (algorithm, hop, n_fft, method)
+                if hop not in (128, 256) or nf not in (512, 1024):
+                    raise ValueError("engine supports n_fft in {512,1024}, hop in {128,256}")
+                noise_key(alg, p, n_frames(L, hop))  # validates the method
+                if (p["noise_method"] == "true_noise" and not with_clean
+                        and n_frames(L, hop) >= 5):
+                    raise ValueError("TrueNoiseEstimator requires clean_audio and noisy_audio")
+                checked.add(ck)
+            by_fft.setdefault(int(nf), []).append((idx, int(sig), alg, p))
         self.plans = [GridPlan(eng, n_fft, S, L, items, with_clean, want_y, want_g, self.y_all,
                                align)
                       for n_fft, items in sorted(by_fft.items())]
@@ -470,12 +493,13 @@ class MultiPlan:
         xst = np.zeros(self.n, dtype=np.int64) if self.align else None
         for p in self.plans:
             s, f, G = p.results()
-            for c, (idx, *_rest) in enumerate(p.items):
-                sse[idx], fin[idx] = s[c], f[c]
-                if gains is not None:
-                    gains[idx] = G[c]
-                if lag is not None and p.lag is not None:
-                    lag[idx], xst[idx] = p.lag[c], p.xstatus[c]
+            ix = p.idx
+            sse[ix], fin[ix] = s, f
+            if gains is not None:
+                for c, i in enumerate(ix):
+                    gains[i] = G[c]
+            if lag is not None and p.lag is not None:
+                lag[ix], xst[ix] = p.lag, p.xstatus
         out = {"sse": sse, "finite": fin}
         if lag is not None:
             out["lag"], out["xcorr_status"] = lag, xst
@@ -493,37 +517,50 @@ def pack_waves(cells, n_fft):
     kernel stages those rows once per workgroup.  Returns (packed cells incl.
     CSE_ALGO_NONE padding, order) with order[i] = index into ``cells`` of packed
     slot i, or -1 for padding.  Groups are ordered longest-first (frames x
-    algorithm cost) so the launch ends on short workgroups; neighbours share
-    rows, and the kernel's XCD remap keeps neighbours on one XCD's L2.
+    algorithm cost, then by key) so the launch ends on short workgroups;
+    neighbours share rows, and the kernel's XCD remap keeps neighbours on one
+    XCD's L2.  Vectorised (numpy): a 100k-cell table packs in milliseconds.
     """
     per = _lib.cells_per_group(n_fft)
-    code_name = {v: k for k, v in _lib.ALGO.items()}
-    groups = {}
-    for i, c in enumerate(cells):
-        key = (int(c["hop"]), int(c["algo"]), int(c["y_offset"]), int(c["noise_offset"]),
-               int(c["noise_stride"]), int(c["clean_offset"]), int(c["lag"]))
-        groups.setdefault(key, []).append(i)
-    slots = []
-    for key, idxs in groups.items():
-        hop, algo = key[0], key[1]
-        cost = (1 + 16000 // hop) * ALGO_COST[code_name[algo]]
-        for s in range(0, len(idxs), per):
-            chunk = idxs[s:s + per]
-            slots.append((-cost, key, chunk + [-1] * (per - len(chunk))))
-    slots.sort(key=lambda w: (w[0], w[1]))
-    order = np.array([i for w in slots for i in w[2]], dtype=np.int64)
+    n = len(cells)
+    if n == 0:
+        return np.zeros(0, dtype=_lib.CELL_DTYPE), np.zeros(0, dtype=np.int64)
+    keys = np.stack([cells[f].astype(np.int64) for f in
+                     ("hop", "algo", "y_offset", "noise_offset", "noise_stride",
+                      "clean_offset", "lag")], axis=1)
+    uniq, inv = np.unique(keys, axis=0, return_inverse=True)  # rows in key order
+    inv = inv.reshape(-1)
+    G = len(uniq)
+    counts = np.bincount(inv, minlength=G)
+    nslots = (counts + per - 1) // per
+    cost_of = np.zeros(8, dtype=np.float64)
+    for name, code in _lib.ALGO.items():
+        if code >= 0:
+            cost_of[code] = ALGO_COST[name]
+    cost = (1 + 16000 // uniq[:, 0]) * cost_of[uniq[:, 1]]
+    gorder = np.lexsort((np.arange(G), -cost))          # longest first, then key order
+    slot_base = np.zeros(G, dtype=np.int64)
+    slot_base[gorder] = np.concatenate([[0], np.cumsum(nslots[gorder])[:-1]])
+    # rank of each cell inside its group, in the cells' original order
+    by_group = np.argsort(inv, kind="stable")
+    first = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    rank = np.empty(n, dtype=np.int64)
+    rank[by_group] = np.arange(n) - first[inv[by_group]]
+    slot = slot_base[inv] + rank // per
+    total = int(nslots.sum())
+    order = np.full(total * per, -1, dtype=np.int64)
+    order[slot * per + rank % per] = np.arange(n)
     packed = np.zeros(len(order), dtype=_lib.CELL_DTYPE)
     real = order >= 0
     packed[real] = cells[order[real]]
-    for g, (_, key, chunk) in enumerate(slots):
-        for s, i in enumerate(chunk):
-            if i < 0:  # padding: same shared rows, no algorithm, no outputs
-                slot = g * per + s
-                packed[slot] = cells[chunk[0]]
-                packed[slot]["algo"] = -1
-                packed[slot]["out_offset"] = -1
-                packed[slot]["gain_offset"] = -1
-    assert all(packed[g * per]["algo"] >= 0 for g in range(len(slots)))
+    # padding: the group's shared rows, no algorithm, no outputs
+    pad = np.nonzero(~real)[0]
+    if len(pad):
+        lead = order[(pad // per) * per]
+        packed[pad] = cells[lead]
+        packed["algo"][pad] = -1
+        packed["out_offset"][pad] = -1
+        packed["gain_offset"][pad] = -1
     return packed, order
 
 

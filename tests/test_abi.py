@@ -87,3 +87,60 @@ def test_wave_packing_groups_and_pads():
         assert slots[0]["algo"] >= 0
     # longest first: hop 128 OMLSA before hop 128 SS and hop 256 OMLSA
     assert packed[0]["algo"] == 3 and packed[0]["hop"] == 128
+
+
+def _pack_waves_loop(cells, n_fft):
+    """Straight per-cell restatement of the slot-group packing (the form the
+    vectorised engine.pack_waves replaced): groups in (-cost, key) order,
+    chunks of CSE_CELLS_PER_GROUP in cell order, padding copies the group's
+    first cell with no algorithm and no outputs."""
+    from classical_speech_enhancement_amd.engine import ALGO_COST
+    per = _lib.cells_per_group(n_fft)
+    code_name = {v: k for k, v in _lib.ALGO.items()}
+    groups = {}
+    for i, c in enumerate(cells):
+        key = tuple(int(c[f]) for f in ("hop", "algo", "y_offset", "noise_offset",
+                                        "noise_stride", "clean_offset", "lag"))
+        groups.setdefault(key, []).append(i)
+    slots = []
+    for key, idxs in groups.items():
+        cost = (1 + 16000 // key[0]) * ALGO_COST[code_name[key[1]]]
+        for s in range(0, len(idxs), per):
+            chunk = idxs[s:s + per]
+            slots.append((-cost, key, chunk + [-1] * (per - len(chunk))))
+    slots.sort(key=lambda w: (w[0], w[1]))
+    order = np.array([i for w in slots for i in w[2]], dtype=np.int64)
+    packed = np.zeros(len(order), dtype=_lib.CELL_DTYPE)
+    real = order >= 0
+    packed[real] = cells[order[real]]
+    for g, (_, key, chunk) in enumerate(slots):
+        for s, i in enumerate(chunk):
+            if i < 0:
+                slot = g * per + s
+                packed[slot] = cells[chunk[0]]
+                packed[slot]["algo"] = -1
+                packed[slot]["out_offset"] = -1
+                packed[slot]["gain_offset"] = -1
+    return packed, order
+
+
+@pytest.mark.parametrize("n_fft", [512, 1024])
+def test_wave_packing_matches_per_cell_form(n_fft):
+    from classical_speech_enhancement_amd.engine import pack_waves
+    rng = np.random.default_rng(n_fft)
+    n = 3000
+    cells = np.zeros(n, dtype=_lib.CELL_DTYPE)
+    cells["algo"] = rng.integers(0, 4, n)
+    cells["hop"] = rng.choice([128, 256], n)
+    cells["y_offset"] = rng.integers(0, 5, n) * 1000
+    cells["noise_offset"] = rng.integers(0, 7, n) * 100
+    cells["noise_stride"] = rng.choice([0, 257], n)
+    cells["clean_offset"] = rng.integers(0, 3, n) * 10
+    cells["lag"] = rng.choice([0, 0, 0, 5, -7], n)
+    cells["out_offset"] = np.arange(n) * 3
+    cells["gain_offset"] = np.arange(n) * 11
+    cells["param"] = rng.random((n, 8)).astype(np.float32)
+    got, go = pack_waves(cells, n_fft)
+    ref, ro = _pack_waves_loop(cells, n_fft)
+    assert np.array_equal(go, ro)
+    assert got.tobytes() == ref.tobytes()

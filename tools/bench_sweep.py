@@ -1,0 +1,60 @@
+"""End-to-end sweep timing on one GPU (GPU box): the reference's main() loop
+body for P synthetic 10-s pairs x the full HEAD grid (both n_fft halves, all
+four algorithms, 9,744 cells per pair): STFT + noise PSDs + fused enhance,
+finalize_enhanced alignment and rescoring, STOI and SNR per cell, and the
+sequential selections — search.run_grid on one rank.
+
+    python tools/bench_sweep.py [--pairs P --reps R]
+
+Prints one JSON line: wall time per sweep with and without STOI, cells/s.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from classical_speech_enhancement_amd import search  # noqa: E402
+from classical_speech_enhancement_amd.engine import Engine  # noqa: E402
+from classical_speech_enhancement_amd.synth import make_pair  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--seconds", type=float, default=10.0)
+    a = ap.parse_args()
+    import torch
+    pairs = [make_pair(200 + i, a.seconds) for i in range(a.pairs)]
+    clean = [c for c, _ in pairs]
+    noisy = [n for _, n in pairs]
+    specs = search.job_specs(a.pairs)
+    eng = Engine()
+    out = {"pairs": a.pairs, "clip_s": a.seconds, "cells": len(specs)}
+    for stoi in (False, True):
+        def compute(c, n, s, ids):
+            return search.engine_compute(c, n, s, ids, engine=eng, stoi=stoi)
+        search.run_grid(clean, noisy, specs, compute=compute)  # warm-up
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            table, best = search.run_grid(clean, noisy, specs, compute=compute)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        key = "with_stoi" if stoi else "snr_only"
+        out[key] = {"s_per_sweep": float(np.median(ts)), "cells_per_s": len(specs) / float(np.median(ts))}
+        if stoi:
+            sb = search.select_best(specs, table, "stoi")
+            out["stoi_winner_mean"] = float(np.mean([v[1] for v in sb.values()]))
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
