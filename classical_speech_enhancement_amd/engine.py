@@ -283,7 +283,8 @@ class GridPlan:
         prm = np.zeros((n, 8), dtype=np.float32)
         for c, (_, _, alg, p) in enumerate(items):
             names = ALGOS[alg][2]
-            prm[c, :len(names)] = [p[k] for k in names]
+            dflt = DEFAULTS.get(alg, {})
+            prm[c, :len(names)] = [p[k] if k in p else dflt[k] for k in names]
         cells["param"] = prm
         self.cells = cells
         packed, self.order = pack_waves(cells, n_fft)
@@ -457,12 +458,7 @@ class MultiPlan:
         checked = set()
         for idx, (sig, alg, params) in enumerate(specs):
             alg = canonical_algo(alg)
-            d = DEFAULTS.get(alg)
-            if d:
-                p = dict(d)
-                p.update(params)
-            else:
-                p = params
+            p = params  # defaults (DEFAULTS) are applied where a value is read
             hop, nf = p["hop_length"], p["n_fft"]
             if not 0 <= int(sig) < S:
                 raise ValueError(f"signal index {sig} out of range")
