@@ -55,6 +55,16 @@ def _cpu_cell(args):
     return 1 + int(len(noisy)) // int(params["hop_length"])
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(budget_s=15.0, seconds=10.0, n_fft=512):
     """The oracle (the reference's algorithm restated, fp64, per-frame Python
     loops, one STFT+estimate per cell exactly like the reference) on the host
@@ -96,6 +106,7 @@ def cpu_baseline(budget_s=15.0, seconds=10.0, n_fft=512):
             else:
                 os.environ[k] = v
     return {"value": units / dt, "unit": "frame-gain evals/s", "cores": cores, "kind": "port",
+            "cpu_model": _cpu_model(),
             "sample": (f"{cells} cells drawn uniformly from the n_fft={n_fft} HEAD grid, "
                        f"one 10-s pair, oracle/ fp64 numpy (reference algorithm incl. per-cell "
                        f"STFT+noise estimate), {cores} single-threaded processes, "
