@@ -270,12 +270,19 @@ struct WG {
     static constexpr int OFF_N = OFF_Y + (CSE_DIRECT_ROWS ? 0 : 2 * YROW);  // float[2][B]
     static constexpr int OFF_C = OFF_N + (CSE_DIRECT_ROWS ? 0 : 2 * NROW);  // float[(waves)][2][HMAX]
     static constexpr int CBUF = 2 * HMAX * 4;                     // one clean double buffer
-    static constexpr int OFF_TW = OFF_C + (CSE_DIRECT_ROWS ? WAVES : 1) * CBUF;  // cf[15][L]
-    static constexpr int OFF_LC = OFF_TW + 15 * G::L * 8;         // cf[L] packing rotor
+    // n_fft 1024 fits 3 workgroups per CU (12 waves instead of 8) by halving
+    // two tables: the pass-1 twiddles keep the 16 lane residues b2, since
+    // e^{2πi (b2 + 16 h2) b/M} = tw[b][b2] W32^{h2 b}; the window keeps slots
+    // q < 16, since slot q + 16 is n + N/2 and w(n + N/2) = 1 - w(n)
+    static constexpr bool HALF_TABLES = (NFFT == 1024);
+    static constexpr int TWL = HALF_TABLES ? 16 : G::L;          // twiddle columns
+    static constexpr int OFF_TW = OFF_C + (CSE_DIRECT_ROWS ? WAVES : 1) * CBUF;  // cf[15][TWL]
+    static constexpr int OFF_LC = OFF_TW + 15 * TWL * 8;          // cf[L] packing rotor
     static constexpr int OFF_CP = OFF_LC + G::L * 8;              // float[CPWG][8] cell params
-    // synthesis window w(n)/NFFT at the lane's 32 sample slots; row stride 36
-    // floats (144 B = 36 banks): the 16 lanes' ds_read_b128 hit disjoint banks
-    static constexpr int WSTR = 36;
+    // synthesis window w(n)/NFFT at the lane's 32 (16) sample slots; row stride
+    // 36 (20) floats: the lanes of a ds_read_b128 group hit disjoint banks
+    static constexpr int WSLOTS = HALF_TABLES ? 16 : 32;
+    static constexpr int WSTR = HALF_TABLES ? 20 : 36;
     static constexpr int OFF_WIN = OFF_CP + CPWG * 32;
     // 1/wss at the lane's 16 retired slots, only for the one R = 2 case
     // (512/256), whose wss is not constant; row stride 20 floats (disjoint banks)
@@ -288,8 +295,8 @@ struct WG {
 // LDS decides how many workgroups share a CU: keep >= 12 waves (3 per SIMD)
 static_assert(CSE_LDS_PAD || (163840 / WG<512>::BYTES) * CSE_WG_WAVES >= 12,
               "n_fft=512 workgroups must fill 12 waves per CU");
-static_assert(CSE_LDS_PAD || (163840 / WG<1024>::BYTES) * CSE_WG_WAVES >= 8,
-              "n_fft=1024 workgroups must fill 8 waves per CU");
+static_assert(CSE_LDS_PAD || (163840 / WG<1024>::BYTES) * CSE_WG_WAVES >= 12,
+              "n_fft=1024 workgroups must fill 12 waves per CU");
 static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
               WG<1024>::CPWG == CSE_CELLS_PER_GROUP(1024), "cse.h slot-group size");
 
@@ -322,6 +329,13 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// window w(n)/NFFT at the lane's slot q (a compile-time index after unrolling)
+template <typename W>
+__device__ __forceinline__ float win_at(const float* wt, int q) {
+    if (W::HALF_TABLES && q >= 16) return (1.0f / (float)W::G::M / 2.0f) - wt[q - 16];
+    return wt[q];
 }
 
 // per-cell parameters as the gain stage wants them
@@ -461,8 +475,8 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 
     // ---- workgroup tables: pass-1 twiddles e^{2πi i b/M} [b-1][i], lane
     // constants [i], cell parameters [slot]
-    for (int e = tid; e < 15 * L; e += W::THREADS) {
-        const int b = 1 + e / L, ii = e % L;
+    for (int e = tid; e < 15 * W::TWL; e += W::THREADS) {
+        const int b = 1 + e / W::TWL, ii = e % W::TWL;
         double s, c;
         sincospi(2.0 * (double)(ii * b) / (double)M, &s, &c);
         ((cf*)(smem + W::OFF_TW))[e] = cmk((float)c, (float)s);
@@ -475,7 +489,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         const int bb = (L == 16) ? ii : (ii & 15), hh = (L == 16) ? 0 : (ii >> 4);
         const int n = SP * (q >> 1) + 2 * bb + 32 * hh + (q & 1);
         const double w = 0.5 - 0.5 * cospi(2.0 * (double)n / (double)NFFT);
-        ((float*)(smem + W::OFF_WIN))[ii * W::WSTR + q] = (float)(w / NFFT);
+        if (q < W::WSLOTS) ((float*)(smem + W::OFF_WIN))[ii * W::WSTR + q] = (float)(w / NFFT);
         if (NFFT == 512 && HOP == 256 && q < 16)
             ((float*)(smem + W::OFF_IWS))[ii * W::ISTR + q] =
                 (float)(1.0 / (0.75 + 0.25 * cospi(2.0 * (double)n / 256.0)));
@@ -689,9 +703,19 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             }
             if (!(CSE_ABLATE & 2)) idft16(z);
             {
-                const cf* tw = (const cf*)((const unsigned char*)tw1 + opaque(8 * i));
+                if constexpr (W::HALF_TABLES) {
+                    const cf* tw = (const cf*)((const unsigned char*)tw1 + opaque(8 * b2));
 #pragma unroll
-                for (int b = 1; b < 16; ++b) z[b] = cmul(z[b], tw[(b - 1) * L]);
+                    for (int b = 1; b < 16; ++b) {
+                        const cf t = tw[(b - 1) * W::TWL];
+                        const cf th = cmul(t, cmk(Rot32::c[b], Rot32::s[b]));  // x W32^b
+                        z[b] = cmul(z[b], h2 ? th : t);
+                    }
+                } else {
+                    const cf* tw = (const cf*)((const unsigned char*)tw1 + opaque(8 * i));
+#pragma unroll
+                    for (int b = 1; b < 16; ++b) z[b] = cmul(z[b], tw[(b - 1) * L]);
+                }
             }
             wave_sync();  // my wave's S reads are issued before the transpose overwrites
             {
@@ -760,10 +784,10 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             const float* wt = (const float*)__builtin_assume_aligned(
                 smem + opaque(W::OFF_WIN + 4 * W::WSTR * i), 16);
 #pragma unroll
-            for (int q = 0; q < F; ++q) done[q] = fmaf(x[q], wt[q], acc[q]);
+            for (int q = 0; q < F; ++q) done[q] = fmaf(x[q], win_at<W>(wt, q), acc[q]);
 #pragma unroll
             for (int q = 0; q < PEND; ++q)
-                acc[q] = fmaf(x[q + F], wt[q + F], q + F < PEND ? acc[q + F] : 0.0f);
+                acc[q] = fmaf(x[q + F], win_at<W>(wt, q + F), q + F < PEND ? acc[q + F] : 0.0f);
         }
         if (valid && !(CSE_ABLATE & 4)) {
             const int o0 = t * HOP + off - NFFT / 2;  // output index of q = 0
@@ -817,7 +841,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                         for (int r = 0; r < R; ++r) {
                             const int tr = t - r;
                             if (tr >= 0 && tr < nf) {
-                                const float w = wt[q + 2 * r * (HOP / SP)] * NFFT;
+                                const float w = win_at<W>(wt, q + 2 * r * (HOP / SP)) * NFFT;
                                 wss = fmaf(w, w, wss);
                             }
                         }

@@ -43,6 +43,12 @@
 
 namespace cse {
 
+// CSE_STOI_ABLATE (timing experiments only; 0 in product builds): skip
+//   1 = resampling arithmetic, 2 = FFT, 4 = band sums, 8 = phase B
+#ifndef CSE_STOI_ABLATE
+#define CSE_STOI_ABLATE 0
+#endif
+
 namespace stoi {
 constexpr int UP = 5, DOWN = 8;          // 10 kHz / 16 kHz
 constexpr int HALF_LEN = 290;            // (581 - 1) / 2
@@ -410,7 +416,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                         uu < 8 * GRP + KN ? cell_sample(y, n, len, lag, clip) : 0.0f;
                 }
                 __syncthreads();
-                if (tid < ns * GRP) {
+                if (tid < ns * GRP && !(CSE_STOI_ABLATE & 1)) {
                     const int s = tid / GRP, g = tid - s * GRP;
                     const int64_t p = L.tab[1 + c0 + s];
                     const int64_t q0 = (HOP * p) / UP;
@@ -448,6 +454,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
             L.ola[hl][n] = v;
         }
         __syncthreads();
+        if (!(CSE_STOI_ABLATE & 2))
         // ---- 512-point rfft of frame fl = [ola[fl], ola[fl+1]] * w, 16 lanes per frame:
         // z[m] = s[2m] + i s[2m+1] (m < 128, 0 above), Z = DFT256(z) as DFT16 x DFT16
         {
@@ -506,7 +513,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
         }
         __syncthreads();
         // ---- band envelopes
-        if (tid < nf * NBAND) {
+        if (tid < nf * NBAND && !(CSE_STOI_ABLATE & 4)) {
             const int fl = tid / NBAND, b = tid - fl * NBAND;
             const double* pw = L.u.pw[fl];
             double s = 0.0;
@@ -605,7 +612,7 @@ __global__ void __launch_bounds__(stoi::NT) stoi_cells_kernel(StoiArgs a) {
     constexpr double clipf = 6.623413251903491;  // 1 + 10^(-BETA/20)
     double dsum = 0.0;
     const int seg = tid & 63, bg = tid >> 6;
-    for (int j0 = 0; j0 < J; j0 += 64) {
+    for (int j0 = 0; j0 < ((CSE_STOI_ABLATE & 8) ? 0 : J); j0 += 64) {
         const int rows = min(64, J - j0) + NSEG - 1;
         __syncthreads();
         for (int i = tid; i < rows * 16; i += NT) {

@@ -55,7 +55,8 @@ def main():
         times.append(e0.elapsed_time(e1))
     ms = float(np.median(times))
     v = out.cpu().numpy()
-    assert np.isfinite(v).all()
+    if not os.environ.get("CSE_BENCH_NOCHECK"):
+        assert np.isfinite(v).all()
     print(json.dumps({"what": "cse_stoi_cells", "cells": a.cells, "clip_s": a.seconds,
                       "ms_per_launch": ms, "cells_per_s": a.cells / (ms / 1e3),
                       "prepare_ms_incl_first_launch": prep_ms, "stoi_mean": float(v.mean())}))
