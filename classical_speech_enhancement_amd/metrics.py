@@ -32,13 +32,23 @@ STOI_SR = 16000
 STOI_CHUNK = 16384
 
 
+_GPU = None
+
+
+def _gpu_visible():
+    global _GPU
+    if _GPU is None:
+        _GPU = bool(torch.cuda.is_available())
+    return _GPU
+
+
 class StoiPlan:
     """Clean side of STOI for S equal-length signals (clean: [S, L] f64 cuda)."""
 
     def __init__(self, clean, sr=STOI_SR):
         if sr != STOI_SR:
             raise NotImplementedError(f"device STOI runs at {STOI_SR} Hz (got sr={sr})")
-        if not torch.cuda.is_available():
+        if not _gpu_visible():
             raise _lib.CseError("no GPU visible: the HIP engine has no CPU fallback")
         self.lib = _lib.load()
         clean = clean.contiguous()

@@ -50,8 +50,9 @@ TOLERANCE = {"stoi": 1e-6, "pesq": 1e-3, "balance": 1e-5, "snr": 1e-5}
 RECORD_FIELDS = ("cell_id", "sse", "snr", "finite", "stoi")  # one float64 row per cell
 TABLE_COLUMN = {"sse": 0, "snr": 1, "finite": 2, "stoi": 3}  # table = records without cell_id
 NCOL = len(RECORD_FIELDS) - 1
-# bound on the cell waveforms held at once for STOI scoring (f32 bytes)
-STOI_WAVE_BYTES = 8 << 30
+# bound on the cell waveforms held at once for STOI scoring (f32 bytes): 32 GB
+# of the 288 GB HBM, i.e. 5 full 10-s pairs (9,744 cells x 640 KB each) per batch
+STOI_WAVE_BYTES = 32 << 30
 
 
 def job_specs(n_pairs, algorithms=None, grids=None, n_fft=None):

@@ -78,3 +78,28 @@ def test_prepare_pair_matches_oracle():
         np.testing.assert_array_equal(nz, ref)
         lag = oracle.align_lag(rc, rn, 16000)
         assert lag == prepare.alignment_lag(rc, rn, 16000)
+
+
+def test_sweep_records_do_not_depend_on_batching():
+    """Per-cell records are the same whether pairs are batched one per plan
+    (the STOI waveform budget forces it) or all together, and on a repeat:
+    no cell's result depends on which other cells share its launch."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from classical_speech_enhancement_amd.engine import Engine
+    clean, noisy = pairs(3, 1.5)
+    specs = search.job_specs(3, grids=SMALL_GRIDS)
+    ids = np.arange(len(specs))
+    eng = Engine()
+    keep = search.STOI_WAVE_BYTES
+    try:
+        search.STOI_WAVE_BYTES = 1
+        a = search.engine_compute(clean, noisy, specs, ids, engine=eng)
+        b = search.engine_compute(clean, noisy, specs, ids, engine=eng)
+        search.STOI_WAVE_BYTES = 1 << 40
+        c = search.engine_compute(clean, noisy, specs, ids, engine=eng)
+    finally:
+        search.STOI_WAVE_BYTES = keep
+    assert np.array_equal(a, b, equal_nan=True)
+    assert np.array_equal(a, c, equal_nan=True)
