@@ -584,7 +584,11 @@ struct StoiArgs {
     double* out;
 };
 
-__global__ void __launch_bounds__(stoi::NT) stoi_cells_kernel(StoiArgs a) {
+// coef is a separate const __restrict__ argument so the compiler can prove it
+// is never written and read it through the scalar cache (s_load): inside the
+// argument struct it became per-lane vector loads waited on right after issue
+__global__ void __launch_bounds__(stoi::NT) stoi_cells_kernel(StoiArgs a,
+                                                              const double* __restrict__ coef) {
     using namespace stoi;
     __shared__ StoiLds L;
     const int64_t c = blockIdx.x;
@@ -603,7 +607,7 @@ __global__ void __launch_bounds__(stoi::NT) stoi_cells_kernel(StoiArgs a) {
     stoi_tables(L);
     double* env = a.scratch + c * a.Mmax * 16;
     const int lag = a.lag ? a.lag[c] : 0;
-    stoi_phase_a<false>(L, a.y + a.y_offset[c], a.len, lag, a.clip != 0, nullptr, a.coef,
+    stoi_phase_a<false>(L, a.y + a.y_offset[c], a.len, lag, a.clip != 0, nullptr, coef,
                         a.btab + (int64_t)sig * a.NBLK * BT, M, env);
     __syncthreads();  // env rows of this workgroup are visible to it
     // ---- phase B: segment j, band b
@@ -745,7 +749,7 @@ extern "C" int cse_stoi_cells(const float* y, const int64_t* y_offset, const int
     a.scratch = (double*)scratch;
     a.out = stoi_out;
     hipLaunchKernelGGL(stoi_cells_kernel, dim3((unsigned)n_cells), dim3(stoi::NT), 0,
-                       (hipStream_t)stream, a);
+                       (hipStream_t)stream, a, a.coef);
     CSE_CHECK_LAUNCH("cse_stoi_cells");
     return CSE_OK;
 }
