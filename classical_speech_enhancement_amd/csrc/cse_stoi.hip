@@ -44,7 +44,8 @@
 namespace cse {
 
 // CSE_STOI_ABLATE (timing experiments only; 0 in product builds): skip
-//   1 = resampling arithmetic, 2 = FFT, 4 = band sums, 8 = phase B
+//   1 = resampling arithmetic, 2 = FFT, 4 = band sums, 8 = phase B,
+//   16 = input loads (staged zeros), 32 = overlap-add
 #ifndef CSE_STOI_ABLATE
 #define CSE_STOI_ABLATE 0
 #endif
@@ -354,7 +355,7 @@ struct StoiLds {
         } b;
     } u;
     double red[stoi::NT / 64];
-    int tab[stoi::BT];
+    int tab[2][stoi::BT];  // this block's table and the next one's (prefetch)
 };
 
 // e (16 kHz) sample n of a cell: the finalize_enhanced output — y shifted by
@@ -390,35 +391,72 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
     using namespace stoi;
     const int tid = threadIdx.x;
     const int nblk = (M + FB - 1) / FB;
+    // 16-kHz input samples of one staging chunk, loaded into registers one
+    // chunk ahead (the global-load latency overlaps the previous chunk's
+    // resampling instead of stalling every chunk)
+    // Loads are unconditional (an out-of-range sample reads y[0] and is
+    // masked off at staging), so the compiler issues all of them back to back
+    // instead of waiting on each inside its branch.
+    constexpr int PF = (SLOTS * SSTR + NT - 1) / NT;
+    float pre[PF];
+    unsigned pmask = 0;
+    auto fetch = [&](const int* tb, int c0) {
+        const int ns = min(SLOTS, tb[0] - c0);
+        pmask = 0;
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int i = tid + u * NT;
+            const int s = i < ns * SSTR ? i / SSTR : 0, uu = i - s * SSTR;
+            const int64_t q0 = ((int64_t)HOP * tb[1 + c0 + s]) / UP;
+            const int64_t n = 8 * q0 + KLO + uu;  // e index (finalize_enhanced output)
+            const int64_t src = n - lag;         // y index
+            const bool ok = i < ns * SSTR && uu < 8 * GRP + KN && n >= 0 && n < len &&
+                            src >= 0 && src < len && !(CSE_STOI_ABLATE & 16);
+            pre[u] = y[ok ? src : 0];
+            pmask |= (ok ? 1u : 0u) << u;
+        }
+    };
+    if (nblk > 0) {
+        __syncthreads();
+        if (tid < BT) L.tab[0][tid] = btab[tid];
+        __syncthreads();
+        if (!PRE) fetch(L.tab[0], 0);
+    }
     for (int blk = 0; blk < nblk; ++blk) {
         const int j0 = blk * FB;
         const int nf = min(FB, M - j0);
-        __syncthreads();  // previous block's readers of tab / union are done
-        if (tid < BT) L.tab[tid] = btab[(int64_t)blk * BT + tid];
-        __syncthreads();
-        const int D = L.tab[0];
-        // ---- 10-kHz half-blocks p = tab[1 + d] into e10[d]
+        const int* tb = L.tab[blk & 1];
+        const int* tn = L.tab[(blk + 1) & 1];
+        __syncthreads();  // previous block's readers of the union and of tn are done
+        if (blk + 1 < nblk && tid < BT) L.tab[(blk + 1) & 1][tid] = btab[(int64_t)(blk + 1) * BT + tid];
+        const int D = tb[0];
+        // ---- 10-kHz half-blocks p = tb[1 + d] into e10[d]
         if (PRE) {
             for (int i = tid; i < D * HOP; i += NT) {
                 const int d = i >> 7, n = i & (HOP - 1);
-                L.u.a.e10[d][n] = x10[(int64_t)L.tab[1 + d] * HOP + n];
+                L.u.a.e10[d][n] = x10[(int64_t)tb[1 + d] * HOP + n];
             }
         } else {
             for (int c0 = 0; c0 < D; c0 += SLOTS) {
                 const int ns = min(SLOTS, D - c0);
                 // stage e[8 q0 - 58 + u], u < 339, at [u & 7][u >> 3]
-                for (int i = tid; i < ns * SSTR; i += NT) {
+#pragma unroll
+                for (int u = 0; u < PF; ++u) {
+                    const int i = tid + u * NT;
                     const int s = i / SSTR, uu = i - s * SSTR;
-                    const int64_t p = L.tab[1 + c0 + s];
-                    const int64_t q0 = (HOP * p) / UP;
-                    const int64_t n = 8 * q0 + KLO + uu;
-                    L.u.a.stage[s * SSTR + (uu & 7) * SROW + (uu >> 3)] =
-                        uu < 8 * GRP + KN ? cell_sample(y, n, len, lag, clip) : 0.0f;
+                    float v = pre[u];
+                    if (clip) v = fminf(fmaxf(v, -1.0f), 1.0f);
+                    if (i < ns * SSTR)
+                        L.u.a.stage[s * SSTR + (uu & 7) * SROW + (uu >> 3)] = ((pmask >> u) & 1) ? v : 0.0f;
                 }
-                __syncthreads();
+                __syncthreads();  // stage (and the next block's table) visible
+                if (c0 + SLOTS < D)
+                    fetch(tb, c0 + SLOTS);
+                else if (blk + 1 < nblk)
+                    fetch(tn, 0);
                 if (tid < ns * GRP && !(CSE_STOI_ABLATE & 1)) {
                     const int s = tid / GRP, g = tid - s * GRP;
-                    const int64_t p = L.tab[1 + c0 + s];
+                    const int64_t p = tb[1 + c0 + s];
                     const int64_t q0 = (HOP * p) / UP;
                     const int64_t q = q0 + g;
                     const float* st = L.u.a.stage + s * SSTR + g;
@@ -445,10 +483,10 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
         }
         __syncthreads();
         // ---- overlap-add: ola[hl][n] = w[n] e10[sa][n] + w[128+n] e10[sb][n]
-        for (int i = tid; i < (nf + 1) * HOP; i += NT) {
+        for (int i = tid; i < ((CSE_STOI_ABLATE & 32) ? 0 : (nf + 1) * HOP); i += NT) {
             const int hl = i >> 7, n = i & (HOP - 1);
-            const int sa = L.tab[1 + MAXD + hl];
-            const int sb = L.tab[1 + MAXD + (FB + 1) + hl];
+            const int sa = tb[1 + MAXD + hl];
+            const int sb = tb[1 + MAXD + (FB + 1) + hl];
             double v = L.wnd[n] * L.u.a.e10[sa][n];
             if (sb >= 0) v = fma(L.wnd[HOP + n], L.u.a.e10[sb][n], v);
             L.ola[hl][n] = v;
