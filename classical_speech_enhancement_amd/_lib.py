@@ -13,6 +13,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CSE_LIB", os.path.join(HERE, "libcse.so"))
 
 CSE_OK = 0
+# ABI revision this package mirrors (cse_version(); CELL_DTYPE == cse_cell_t,
+# NOISE_JOB_DTYPE == cse_noise_job_t, NoiseParams == cse_noise_params_t)
+ABI_VERSION = 4
 ALGO = {"NONE": -1, "SS": 0, "WIENER": 1, "MMSE": 2, "OMLSA": 3}
 NOISE = {"percentile": 0, "min_tracking": 1, "true_noise": 2}
 
@@ -31,8 +34,20 @@ NOISE_JOB_DTYPE = np.dtype([
     ("out_frames", np.int32), ("mu", np.float64), ("inv_eps", np.float64)], align=True)
 assert NOISE_JOB_DTYPE.itemsize == 40
 
+
+class NoiseParams(ctypes.Structure):
+    """cse_noise_params_t: estimator constructor parameters
+    (noise_estimation.py:12-13, :60) and the TrueNoise frame fit (:149-153)."""
+    _fields_ = [("percentile", ctypes.c_double), ("max_fraction", ctypes.c_double),
+                ("floor_rel", ctypes.c_double), ("smoothing_factor", ctypes.c_double),
+                ("min_frames", ctypes.c_int32), ("adaptive_short", ctypes.c_int32),
+                ("window_size", ctypes.c_int32), ("src_frames", ctypes.c_int32)]
+
+
+assert ctypes.sizeof(NoiseParams) == 48
+
 EXPORTS = ("cse_version", "cse_last_error", "cse_cells_per_group", "cse_stft",
-           "cse_noise_workspace_bytes",
+           "cse_noise_workspace_bytes", "cse_noise_default_params", "cse_noise_estimate_ex",
            "cse_noise_estimate", "cse_noise_smooth", "cse_noise_median",
            "cse_noise_percentile_med", "cse_noise_min_tracking_med", "cse_noise_finish",
            "cse_noise_invert", "cse_istft_norm", "cse_enhance_cells",
@@ -77,6 +92,10 @@ def load(path=LIB_PATH):
     lib.cse_stft.argtypes = [P, P, i64, i64, i32, i32, P, P, P]
     lib.cse_noise_workspace_bytes.restype = i64
     lib.cse_noise_workspace_bytes.argtypes = [i64, i32, i32]
+    lib.cse_noise_default_params.restype = None
+    lib.cse_noise_default_params.argtypes = [P]
+    lib.cse_noise_estimate_ex.restype = i32
+    lib.cse_noise_estimate_ex.argtypes = [i32, P, i64, i32, i32, P, f64, P, P, P]
     lib.cse_noise_estimate.restype = i32
     lib.cse_noise_estimate.argtypes = [i32, P, i64, i32, i32, f64, f64, P, P, P]
     lib.cse_noise_smooth.restype = i32
@@ -109,6 +128,16 @@ def load(path=LIB_PATH):
     lib.cse_stoi_cells.argtypes = [P, P, P, P, i64, i64, i64, i32, P, P, P, P]
     lib.cse_enhance_cells.restype = i32
     lib.cse_enhance_cells.argtypes = [i32, i64, P, i64, P, P, P, P, i64, P, P, P, P]
+    # the kernels read the cell/job tables laid out as this package packs them:
+    # refuse a library of another ABI revision.  The packer (engine.pack_waves)
+    # takes the slot-group size from the library itself; it must be usable.
+    ver = lib.cse_version()
+    if ver != ABI_VERSION:
+        raise CseError(f"{path}: ABI version {ver}, this package mirrors {ABI_VERSION} (rebuild)")
+    for n_fft in (512, 1024):
+        per = lib.cse_cells_per_group(n_fft)
+        if per <= 0 or per % 2:
+            raise CseError(f"{path}: {per} cells per slot group at n_fft={n_fft}")
     _lib = lib
     return lib
 

@@ -2,7 +2,7 @@
 //
 //   PercentileNoiseEstimator.estimate   :20-56   -> frame_energy + select_quiet + bin_stats
 //   MinTrackingNoiseEstimator.estimate  :64-95   -> bin_stats(median) + iir + min_filter
-//   TrueNoiseEstimator.estimate         :115-155 -> floor_cast on |STFT(noisy-clean)|^2
+//   TrueNoiseEstimator.estimate         :115-155 -> true_fit on |STFT(noisy-clean)|^2
 //   _simple_noise_estimate              :226-232 -> bin_stats(simple) when T < 5
 //   noise smoothing (mmse.py:48-54, advanced_mmse.py:60-66) -> smooth_kernel
 //
@@ -242,10 +242,16 @@ __global__ void min_filter_kernel(const double* __restrict__ S, int T, int B, in
     }
 }
 
-__global__ void floor_cast_kernel(const double* __restrict__ P, int64_t n, double eps,
-                                  float* __restrict__ N) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) N[i] = (float)fmax(P[i], eps);
+// TrueNoise frame fit (noise_estimation.py:146-153): max(P, eps), rows past
+// the source's last frame repeat it (np.pad mode='edge'), extra rows trimmed
+__global__ void true_fit_kernel(const double* __restrict__ P, int T_src, int T, int B, double eps,
+                                float* __restrict__ N) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.y;
+    const int64_t sig = blockIdx.z;
+    if (b >= B) return;
+    const int ts = t < T_src ? t : T_src - 1;
+    N[(sig * T + t) * (int64_t)B + b] = (float)fmax(P[(sig * T_src + ts) * (int64_t)B + b], eps);
 }
 
 __global__ void smooth_kernel(const float* __restrict__ N, int T, int B, int src_frames,
@@ -340,11 +346,12 @@ static Workspace carve(void* ws, int64_t n_sig, int T, int B) {
     return w;
 }
 
-// (k, percentile) exactly as noise_estimation.py:29-41
-static void quiet_count(int T, double pct_in, int* k_out, double* pct_out) {
-    int min_frames = 10;
-    double pct = pct_in;
-    if (T < 30) {
+// (k, percentile) exactly as noise_estimation.py:29-41 (constructor
+// parameters :12-13: min_frames, max_fraction, adaptive_short)
+static void quiet_count(int T, const cse_noise_params_t& prm, int* k_out, double* pct_out) {
+    int min_frames = prm.min_frames;
+    double pct = prm.percentile;
+    if (prm.adaptive_short && T < 30) {
         min_frames = (T / 4 > 2) ? T / 4 : 2;
         const int target = ((int)(T * 0.15) > 3) ? (int)(T * 0.15) : 3;
         pct = 100.0 * target / T;
@@ -352,7 +359,7 @@ static void quiet_count(int T, double pct_in, int* k_out, double* pct_out) {
     }
     int k = (int)ceil((double)T * (pct / 100.0));
     if (k < min_frames) k = min_frames;
-    int cap = (int)ceil((double)T * 0.30);
+    int cap = (int)ceil((double)T * prm.max_fraction);
     if (cap < 1) cap = 1;
     if (k > cap) k = cap;
     if (k > T) k = T;
@@ -381,11 +388,11 @@ static int launch_simple(const double* P, int64_t n_sig, int T, int B, double ep
 }
 
 static int launch_percentile(const double* P, const double* med, int64_t n_sig, int T, int B,
-                             double percentile, double eps, float* N, Workspace w,
+                             const cse_noise_params_t& prm, double eps, float* N, Workspace w,
                              hipStream_t s) {
     int k;
     double pct;
-    quiet_count(T, percentile, &k, &pct);
+    quiet_count(T, prm, &k, &pct);
     const int n2_all = next_pow2(T), n2_sel = next_pow2(k);
     hipLaunchKernelGGL(frame_energy_kernel, dim3(T, (unsigned)n_sig), dim3(256), 0, s, P, T, B,
                        eps, w.energy);
@@ -394,17 +401,21 @@ static int launch_percentile(const double* P, const double* med, int64_t n_sig, 
                        w.sel);
     hipLaunchKernelGGL(bin_stats_kernel, dim3(B, (unsigned)n_sig), dim3(256),
                        (size_t)n2_sel * sizeof(double), s, P, T, B, n2_all,
-                       (int)STATS_PERCENTILE, (const int*)w.sel, k, n2_sel, pct / 100.0, 0.02,
+                       (int)STATS_PERCENTILE, (const int*)w.sel, k, n2_sel, pct / 100.0, prm.floor_rel,
                        eps, (double*)med, N, 0);
     CSE_CHECK_LAUNCH("noise percentile");
     return CSE_OK;
 }
 
 static int launch_min_tracking(const double* P, const double* med, int64_t n_sig, int T, int B,
-                               double eps, float* N, double eps_b, float* Nb, Workspace w,
-                               hipStream_t s) {
-    const double a = fmax(0.8, fmin(0.95, 1.0 - 5.0 / (double)T));
-    int win = T < 50 ? T : 50;  // min(max(3, 50), T), made odd
+                               const cse_noise_params_t& prm, double eps, float* N, double eps_b,
+                               float* Nb, Workspace w, hipStream_t s) {
+    // alpha: smoothing_factor, or max(0.8, min(0.95, 1 - 5/T)) when None (:72-75)
+    const double a = (prm.smoothing_factor == prm.smoothing_factor)
+                         ? prm.smoothing_factor
+                         : fmax(0.8, fmin(0.95, 1.0 - 5.0 / (double)T));
+    int win = prm.window_size > 3 ? prm.window_size : 3;  // min(max(3, w), T), made odd (:97-99)
+    if (win > T) win = T;
     if (win % 2 == 0) win += 1;
     hipLaunchKernelGGL(iir_kernel, dim3(ceil_div(B, 64), (unsigned)n_sig), dim3(64), 0, s, P, T, B,
                        a, w.S);
@@ -446,16 +457,29 @@ extern "C" int64_t cse_noise_workspace_bytes(int64_t n_sig, int T, int B) {
            align256(n_sig * (int64_t)B * 8) + align256(n_sig * (int64_t)T * B * 8);
 }
 
-extern "C" int cse_noise_estimate(int method, const double* P, int64_t n_sig, int T, int B,
-                                  double percentile, double eps, float* N, void* workspace,
-                                  cse_stream_t stream) {
+extern "C" void cse_noise_default_params(cse_noise_params_t* prm) {
+    if (!prm) return;
+    prm->percentile = 20.0;
+    prm->max_fraction = 0.30;
+    prm->floor_rel = 0.02;
+    prm->smoothing_factor = __builtin_nan("");
+    prm->min_frames = 10;
+    prm->adaptive_short = 1;
+    prm->window_size = 50;
+    prm->src_frames = 0;
+}
+
+extern "C" int cse_noise_estimate_ex(int method, const double* P, int64_t n_sig, int T, int B,
+                                     const cse_noise_params_t* prm, double eps, float* N,
+                                     void* workspace, cse_stream_t stream) {
     hipStream_t s = (hipStream_t)stream;
     CSE_NOISE_SHAPE_CHECKS("cse_noise_estimate");
-    CSE_CHECK_ARG(N != nullptr, "cse_noise_estimate: N is NULL");
+    CSE_CHECK_ARG(N != nullptr && prm != nullptr, "cse_noise_estimate: N or params is NULL");
     if (method == CSE_NOISE_TRUE) {
-        const int64_t n = n_sig * (int64_t)T * B;
-        hipLaunchKernelGGL(floor_cast_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, s, P, n, eps,
-                           N);
+        const int T_src = prm->src_frames > 0 ? prm->src_frames : T;
+        CSE_CHECK_ARG(T_src <= (1 << 24), "cse_noise_estimate: src_frames=%d", T_src);
+        hipLaunchKernelGGL(true_fit_kernel, dim3(ceil_div(B, 256), T, (unsigned)n_sig), dim3(256),
+                           0, s, P, T_src, T, B, eps, N);
         CSE_CHECK_LAUNCH("cse_noise_estimate(true)");
         return CSE_OK;
     }
@@ -470,8 +494,17 @@ extern "C" int cse_noise_estimate(int method, const double* P, int64_t n_sig, in
     rc = launch_median(P, n_sig, T, B, w.med, s);
     if (rc) return rc;
     if (method == CSE_NOISE_PERCENTILE)
-        return launch_percentile(P, w.med, n_sig, T, B, percentile, eps, N, w, s);
-    return launch_min_tracking(P, w.med, n_sig, T, B, eps, N, 0.0, nullptr, w, s);
+        return launch_percentile(P, w.med, n_sig, T, B, *prm, eps, N, w, s);
+    return launch_min_tracking(P, w.med, n_sig, T, B, *prm, eps, N, 0.0, nullptr, w, s);
+}
+
+extern "C" int cse_noise_estimate(int method, const double* P, int64_t n_sig, int T, int B,
+                                  double percentile, double eps, float* N, void* workspace,
+                                  cse_stream_t stream) {
+    cse_noise_params_t prm;
+    cse_noise_default_params(&prm);
+    prm.percentile = percentile;
+    return cse_noise_estimate_ex(method, P, n_sig, T, B, &prm, eps, N, workspace, stream);
 }
 
 extern "C" int cse_noise_median(const double* P, int64_t n_sig, int T, int B, double* med,
@@ -491,8 +524,11 @@ extern "C" int cse_noise_percentile_med(const double* P, const double* med, int6
     CSE_CHECK_ARG(T >= 5, "cse_noise_percentile_med: T=%d < 5 (use the simple estimate)", T);
     int rc = reserve_lds();
     if (rc) return rc;
-    return launch_percentile(P, med, n_sig, T, B, percentile, eps, N,
-                             carve(workspace, n_sig, T, B), (hipStream_t)stream);
+    cse_noise_params_t prm;
+    cse_noise_default_params(&prm);
+    prm.percentile = percentile;
+    return launch_percentile(P, med, n_sig, T, B, prm, eps, N, carve(workspace, n_sig, T, B),
+                             (hipStream_t)stream);
 }
 
 extern "C" int cse_noise_min_tracking_med(const double* P, const double* med, int64_t n_sig,
@@ -501,7 +537,9 @@ extern "C" int cse_noise_min_tracking_med(const double* P, const double* med, in
     CSE_NOISE_SHAPE_CHECKS("cse_noise_min_tracking_med");
     CSE_CHECK_ARG(med && N && workspace, "cse_noise_min_tracking_med: NULL pointer");
     CSE_CHECK_ARG(T >= 5, "cse_noise_min_tracking_med: T=%d < 5 (use the simple estimate)", T);
-    return launch_min_tracking(P, med, n_sig, T, B, eps, N, eps_b, N_b,
+    cse_noise_params_t prm;
+    cse_noise_default_params(&prm);
+    return launch_min_tracking(P, med, n_sig, T, B, prm, eps, N, eps_b, N_b,
                                carve(workspace, n_sig, T, B), (hipStream_t)stream);
 }
 

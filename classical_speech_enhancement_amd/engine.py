@@ -102,6 +102,27 @@ def noise_key(alg, params, T):
     return (method, pct, eps, expand, mu, code != "SS")
 
 
+NOISE_PARAM_KEYS = ("percentile", "min_frames", "max_fraction", "floor_rel", "adaptive_short",
+                    "window_size", "smoothing_factor")
+
+
+def noise_params(percentile=20.0, min_frames=10, max_fraction=0.30, floor_rel=0.02,
+                 adaptive_short=True, window_size=50, smoothing_factor=None, src_frames=0):
+    """cse_noise_params_t from the reference's estimator constructor arguments
+    (PercentileNoiseEstimator noise_estimation.py:12-13, MinTrackingNoiseEstimator
+    :60; defaults as there).  smoothing_factor None -> NaN."""
+    prm = _lib.NoiseParams()
+    prm.percentile = float(percentile)
+    prm.max_fraction = float(max_fraction)
+    prm.floor_rel = float(floor_rel)
+    prm.smoothing_factor = math.nan if smoothing_factor is None else float(smoothing_factor)
+    prm.min_frames = int(min_frames)
+    prm.adaptive_short = 1 if adaptive_short else 0
+    prm.window_size = int(window_size)
+    prm.src_frames = int(src_frames)
+    return prm
+
+
 def key_is_static(key):
     method, _, _, expand, mu, _ = key
     return method in ("percentile", "simple") and not expand and mu is None
@@ -127,8 +148,15 @@ class Engine:
                                      _stream()), "cse_stft")
         return Y, P
 
-    def noise_estimate(self, method, P, percentile=20.0, eps=1e-10, out=None):
-        S, T, B = P.shape
+    def noise_estimate(self, method, P, percentile=20.0, eps=1e-10, out=None, frames=None,
+                       **params):
+        """cse_noise_estimate_ex on P [S, T', B] f64.  params: estimator
+        constructor parameters (min_frames, max_fraction, floor_rel,
+        adaptive_short, window_size, smoothing_factor; noise_estimation.py:12-13,
+        :60).  true_noise: P is the power of STFT(noisy - clean) over the
+        shorter length, fit to ``frames`` (default T') frames (:149-153)."""
+        S, Tp, B = P.shape
+        T = Tp if frames is None else int(frames)
         code = {"percentile": 0, "min_tracking": 1, "true_noise": 2, "simple": 0}[method]
         static = method == "percentile" or (T < 5 and method != "true_noise")
         shape = (S, B) if (static and method != "min_tracking") else (S, T, B)
@@ -136,8 +164,11 @@ class Engine:
             out = torch.empty(shape, dtype=torch.float32, device=P.device)
         ws = torch.empty(int(self.lib.cse_noise_workspace_bytes(S, T, B)), dtype=torch.uint8,
                          device=P.device)
-        _lib.check(self.lib.cse_noise_estimate(code, _ptr(P), S, T, B, float(percentile),
-                                               float(eps), _ptr(out), _ptr(ws), _stream()),
+        prm = noise_params(percentile=percentile, src_frames=Tp if code == 2 else 0, **params)
+        if code != 2 and Tp != T:
+            raise ValueError("frames applies to true_noise only")
+        _lib.check(self.lib.cse_noise_estimate_ex(code, _ptr(P), S, T, B, ctypes.byref(prm),
+                                                  float(eps), _ptr(out), _ptr(ws), _stream()),
                    f"cse_noise_estimate({method})")
         return out
 
@@ -159,12 +190,13 @@ class Engine:
 
     # ------------------------------------------------------------------ grid
     def plan(self, n_signals, length, specs, with_clean=True, want_waveforms=False,
-             want_gains=False, align=False):
+             want_gains=False, align=False, true_len=None):
         """Build one GridPlan per n_fft for these specs (see GridPlan)."""
         return MultiPlan(self, n_signals, length, specs, with_clean, want_waveforms, want_gains,
-                         align)
+                         align, true_len)
 
-    def run(self, noisy, specs, clean=None, want_waveforms=False, want_gains=False, align=False):
+    def run(self, noisy, specs, clean=None, want_waveforms=False, want_gains=False, align=False,
+            true_len=None):
         """Enhance every cell spec; returns a dict of per-spec results.
 
         noisy/clean: [S, L] float64 cuda tensors (clean may be None if no spec
@@ -172,9 +204,13 @@ class Engine:
         (signal_index, algorithm_name, params).  Results (spec order):
           sse [n] f64 numpy, finite [n] bool numpy, and optionally
           'y' [n, L] f32 cuda and 'G' list of [T, B] f32 cuda.
+        true_len: TrueNoise estimates use the first true_len samples of noisy
+        and clean (a clean reference shorter than the noisy signal,
+        noise_estimation.py:128-130); default L.
         """
         S, L = noisy.shape
-        mp = self.plan(S, L, specs, clean is not None, want_waveforms, want_gains, align)
+        mp = self.plan(S, L, specs, clean is not None, want_waveforms, want_gains, align,
+                       true_len)
         mp.execute(noisy, clean)
         return mp.results()
 
@@ -193,8 +229,11 @@ class GridPlan:
     """
 
     def __init__(self, eng, n_fft, S, L, items, with_clean, want_y, want_g, y_all=None,
-                 align=False):
+                 align=False, true_len=None):
         self.eng, self.n_fft, self.S, self.L = eng, n_fft, S, L
+        self.true_len = L if true_len is None else int(true_len)
+        if not 1 <= self.true_len <= L:
+            raise ValueError(f"true_len={self.true_len} not in [1, {L}]")
         self.items = items
         dev = eng.device
         B = self.B = n_fft // 2 + 1
@@ -244,7 +283,8 @@ class GridPlan:
             if method == "true_noise" and hop not in self.Ptrue:
                 if not with_clean:
                     raise ValueError("TrueNoiseEstimator requires clean_audio and noisy_audio")
-                self.Ptrue[hop] = torch.empty((S, T, B), dtype=torch.float64, device=dev)
+                self.Ptrue[hop] = torch.empty((S, n_frames(self.true_len, hop), B),
+                                              dtype=torch.float64, device=dev)
         self.pool = torch.empty(noff, dtype=torch.float32, device=dev)
         self.raw = torch.empty(max(roff, 1), dtype=torch.float32, device=dev)
         jt = np.zeros(len(jobs), dtype=_lib.NOISE_JOB_DTYPE)
@@ -332,7 +372,11 @@ class GridPlan:
             _lib.check(lib.cse_stft(_ptr(noisy), None, S, L, self.n_fft, hop, _ptr(yv),
                                     _ptr(self.P[hop]), st), "cse_stft")
             if hop in self.Ptrue:
-                _lib.check(lib.cse_stft(_ptr(noisy), _ptr(clean), S, L, self.n_fft, hop, None,
+                m = self.true_len
+                xn, xc = noisy, clean
+                if m < L:  # the STFT of the trimmed difference (noise_estimation.py:128-133)
+                    xn, xc = noisy[:, :m].contiguous(), clean[:, :m].contiguous()
+                _lib.check(lib.cse_stft(_ptr(xn), _ptr(xc), S, m, self.n_fft, hop, None,
                                         _ptr(self.Ptrue[hop]), st), "cse_stft(true)")
             bases = [b for b in self.raw_off if b[0] == hop]
             P = self.P[hop]
@@ -361,8 +405,10 @@ class GridPlan:
                                                       _ptr(raw(b)), _ptr(self.ws), st),
                                "cse_noise_estimate(simple)")
                 elif method == "true_noise":
-                    _lib.check(lib.cse_noise_estimate(2, _ptr(self.Ptrue[hop]), S, T, B, 0.0,
-                                                      float(eps), _ptr(raw(b)), None, st),
+                    prm = noise_params(src_frames=self.Ptrue[hop].shape[1])
+                    _lib.check(lib.cse_noise_estimate_ex(2, _ptr(self.Ptrue[hop]), S, T, B,
+                                                         ctypes.byref(prm), float(eps),
+                                                         _ptr(raw(b)), None, st),
                                "cse_noise_estimate(true)")
         _lib.check(lib.cse_noise_finish(_ptr(self.jobs_d), self.n_jobs, S, B, _ptr(self.raw),
                                         _ptr(self.pool), st), "cse_noise_finish")
@@ -448,7 +494,7 @@ class GridPlan:
 class MultiPlan:
     """GridPlans for every n_fft present in a spec list (spec order preserved)."""
 
-    def __init__(self, eng, S, L, specs, with_clean, want_y, want_g, align=False):
+    def __init__(self, eng, S, L, specs, with_clean, want_y, want_g, align=False, true_len=None):
         self.n = len(specs)
         self.align = align
         self.want_g = want_g
@@ -473,7 +519,7 @@ class MultiPlan:
                 checked.add(ck)
             by_fft.setdefault(int(nf), []).append((idx, int(sig), alg, p))
         self.plans = [GridPlan(eng, n_fft, S, L, items, with_clean, want_y, want_g, self.y_all,
-                               align)
+                               align, true_len)
                       for n_fft, items in sorted(by_fft.items())]
         self.units = sum(p.units for p in self.plans)
 

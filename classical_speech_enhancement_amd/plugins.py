@@ -16,7 +16,7 @@ these raise.
 import numpy as np
 import torch
 
-from .engine import Engine, n_frames
+from .engine import NOISE_PARAM_KEYS, Engine, n_frames
 
 _ENGINE = None
 
@@ -47,16 +47,22 @@ def _single(alg, noisy, clean, params, rule):
     if x.size == 0:  # the reference's reflect padding of an empty signal raises
         raise ValueError("can't extend empty axis 0 using modes other than 'constant' or 'empty'")
     eng = engine()
-    c = None
+    c, m = None, None
     if clean is not None and params.get("noise_method") == "true_noise":
         cl = np.asarray(clean, dtype=np.float64)
-        m = min(len(cl), len(x))  # TrueNoiseEstimator trims to the shorter (:128-130)
+        # TrueNoiseEstimator trims both to the shorter (noise_estimation.py:128-130),
+        # takes the STFT of the difference and edge-pads its frames to the
+        # noisy signal's (:149-153): the engine's true_len
+        m = min(len(cl), len(x))
+        if m == 0:
+            if n_frames(len(x), params["hop_length"]) >= 5:  # below 5 frames no estimator runs
+                # librosa.stft of the empty difference signal raises
+                raise ValueError("can't extend empty axis 0 using modes other than 'constant' or 'empty'")
         c = np.zeros_like(x)
         c[:m] = cl[:m]
-        if m < len(x):
-            raise NotImplementedError("true_noise with clean shorter than noisy (frame edge-pad)")
+        m = m or None
     res = eng.run(_dev(x), [(0, alg, params)], clean=None if c is None else _dev(c),
-                  want_waveforms=True)
+                  want_waveforms=True, true_len=m)
     return res["y"][0].cpu().numpy().astype(np.float64)
 
 
@@ -96,40 +102,48 @@ def advanced_mmse(noisy_audio, sr, n_fft, hop_length, alpha, ksi_min, q, noise_m
 def noise_estimation(y, sr, method="percentile", n_fft=1024, hop_length=256, win_length=None,
                      estimator_params=None, window="hann", center=True, pad_mode="reflect",
                      **kwargs):
-    """Noise PSD (B,1) or (B,T) float64, like noise_estimation.py:158-212."""
+    """Noise PSD (B,1) or (B,T) float64, like noise_estimation.py:158-212.
+
+    Argument flow as there: the estimator is constructed from
+    {**estimator_params, **kwargs} (:175, :197; percentile, min_frames,
+    max_fraction, floor_rel, adaptive_short, window_size, smoothing_factor),
+    while estimate() reads eps and clean_audio from **kwargs only (:199-210):
+    eps defaults to 1e-10 (percentile, min_tracking) / 1e-12 (true_noise), the
+    T < 5 fallback reads eps from the merged dict (:191-195)."""
     if window != "hann" or not center or pad_mode != "reflect" or (win_length or n_fft) != n_fft:
         raise NotImplementedError("only hann/center/reflect/win_length=n_fft is implemented")
-    params = dict(estimator_params or {})
-    params.update(kwargs)
-    unsupported = {k for k in params if k not in ("percentile", "eps", "clean_audio")}
-    if unsupported:
-        raise NotImplementedError(f"non-default estimator parameters {sorted(unsupported)}")
+    full = dict(estimator_params or {})
+    full.update(kwargs)
+    ctor = {k: full[k] for k in NOISE_PARAM_KEYS if k in full}
     x = np.asarray(y, dtype=np.float64)
     if x.ndim > 1:
         x = x.mean(axis=1)
+    if x.size == 0:  # librosa's reflect padding of an empty signal raises
+        raise ValueError("can't extend empty axis 0 using modes other than 'constant' or 'empty'")
     eng = engine()
     xd = _dev(x)
-    eps = params.get("eps", 1e-10)
     T = n_frames(len(x), hop_length)
     if T < 5:
         _, P = eng.stft(xd, n_fft, hop_length, want_y=False)
-        N = eng.noise_estimate("percentile", P, 25.0, eps)
+        N = eng.noise_estimate("percentile", P, 25.0, full.get("eps", 1e-10))
         return N[0].cpu().numpy().astype(np.float64)[:, None]
     if method == "percentile":
         _, P = eng.stft(xd, n_fft, hop_length, want_y=False)
-        N = eng.noise_estimate("percentile", P, params.get("percentile", 20.0), eps)
+        N = eng.noise_estimate("percentile", P, eps=kwargs.get("eps", 1e-10), **ctor)
         return N[0].cpu().numpy().astype(np.float64)[:, None]
     if method == "min_tracking":
         _, P = eng.stft(xd, n_fft, hop_length, want_y=False)
-        return eng.noise_estimate("min_tracking", P, eps=eps)[0].cpu().numpy().astype(np.float64).T
+        N = eng.noise_estimate("min_tracking", P, eps=kwargs.get("eps", 1e-10), **ctor)
+        return N[0].cpu().numpy().astype(np.float64).T
     if method == "true_noise":
-        clean = params.get("clean_audio")
+        clean = kwargs.get("clean_audio")
         if clean is None:
             raise ValueError("TrueNoiseEstimator requires clean_audio and noisy_audio")
-        c = np.zeros_like(x)
-        m = min(len(c), len(clean))
-        c[:m] = np.asarray(clean, dtype=np.float64)[:m]
-        _, P = eng.stft(xd, n_fft, hop_length, x_sub=_dev(c), want_y=False)
-        out = eng.noise_estimate("true_noise", P, eps=params.get("eps", 1e-12))
+        clean = np.asarray(clean, dtype=np.float64)
+        m = min(len(clean), len(x))  # :128-130
+        if m == 0:
+            raise ValueError("can't extend empty axis 0 using modes other than 'constant' or 'empty'")
+        _, P = eng.stft(_dev(x[:m]), n_fft, hop_length, x_sub=_dev(clean[:m]), want_y=False)
+        out = eng.noise_estimate("true_noise", P, eps=kwargs.get("eps", 1e-12), frames=T)
         return out[0].cpu().numpy().astype(np.float64).T
     raise ValueError(f"Unbekannte Methode: {method}")

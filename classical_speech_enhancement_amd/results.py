@@ -13,10 +13,13 @@ The reference's batch driver writes (speech_enhancement_comparison.py):
 
 The device scores STOI (pystoi 0.4.1 restated, metrics.py) and SNR; the pesq
 extension is not in this image, so the PESQ fields are None
-("NA" in the CSV).  The STOI-optimal cell fills the `*_stoiopt` STOI/SNR
-columns and `best_params_stoi`; the SNR-optimal cell fills the `*_balopt`
-SNR column and `best_params_snr`.  Every key of the reference row is present,
-so readers of all_results.json keep working.
+("NA" in the CSV), and so is everything the balance objective
+(calculate_combined_speech_score of STOI and PESQ) selects: snr_balopt,
+stoi_balopt, pesq_balopt, best_params_balanced stay None/{} — every reference
+key keeps the reference's meaning.  The STOI-optimal cell fills the `*_stoiopt`
+STOI/SNR columns and `best_params_stoi`.  The SNR-optimal cell, which the
+reference does not select, is reported under keys of its own: snr_snropt and
+best_params_snr (and snr_snropt_mean in summary_means.json).
 """
 
 import json
@@ -37,7 +40,7 @@ SUMMARY_KEYS = (("stoi_noisy_mean", "stoi_noisy"), ("pesq_noisy_mean", "pesq_noi
                 ("stoi_stoiopt_mean", "stoi_stoiopt"), ("pesq_stoiopt_mean", "pesq_stoiopt"),
                 ("stoi_pesqopt_mean", "stoi_pesqopt"), ("pesq_pesqopt_mean", "pesq_pesqopt"),
                 ("stoi_balopt_mean", "stoi_balopt"), ("pesq_balopt_mean", "pesq_balopt"),
-                ("snr_balopt_mean", "snr_balopt"))
+                ("snr_balopt_mean", "snr_balopt"), ("snr_snropt_mean", "snr_snropt"))
 
 
 def result_row(stem, alg, sr, snr_noisy, best_snr, best_params, stoi_noisy=None,
@@ -45,13 +48,14 @@ def result_row(stem, alg, sr, snr_noisy, best_snr, best_params, stoi_noisy=None,
     """One all_results.json row (run_algorithm_on_pair :314-338).  STOI
     fields come from the device STOI (the STOI-optimal cell fills
     stoi_stoiopt / snr_stoiopt / best_params_stoi); PESQ fields are None (no
-    pesq extension), so the PESQ-opt and balance columns stay None except
-    snr_balopt, which carries the SNR-optimal cell (also snr_snropt /
-    best_params_snr)."""
+    pesq extension), and so are the PESQ-opt and balance-opt columns
+    (:320-333: the balance objective needs PESQ).  The SNR-optimal cell goes
+    to the extra keys snr_snropt / best_params_snr only."""
     row = {k: None for k in ROW_KEYS}
-    row.update(alg=alg, stem=stem, sr=int(sr), snr_noisy=snr_noisy, snr_balopt=best_snr,
+    row.update(alg=alg, stem=stem, sr=int(sr), snr_noisy=snr_noisy,
                best_params_stoi=dict(stoi_params or {}), best_params_pesq={},
-               best_params_balanced={}, snr_snropt=best_snr, best_params_snr=dict(best_params or {}),
+               best_params_balanced={}, snr_snropt=best_snr,
+               best_params_snr=dict(best_params or {}),
                stoi_noisy=stoi_noisy, stoi_stoiopt=stoi_best, snr_stoiopt=snr_stoiopt)
     return row
 

@@ -168,13 +168,15 @@ def gather_records(local, n_total, group=None, device=None):
     rows padded to the largest shard so one all_gather_into_tensor moves them."""
     import torch
     import torch.distributed as dist
-    if group is None and not (dist.is_available() and dist.is_initialized()):
-        world = 1
-    else:
-        world = dist.get_world_size(group)
+    dist_on = group is not None or (dist.is_available() and dist.is_initialized())
+    world = dist.get_world_size(group) if dist_on else 1
+    if dist_on:
+        if device is None and dist.get_backend(group) == "nccl":
+            # RCCL moves device tensors only: gather on this rank's GPU
+            device = torch.device("cuda", torch.cuda.current_device())
     width = 1 + NCOL
     rec = torch.as_tensor(np.asarray(local, dtype=np.float64).reshape(-1, width))
-    if world > 1:
+    if dist_on:  # the collective runs at any world size, 1 included
         n = torch.tensor([rec.shape[0]], dtype=torch.int64, device=device)
         counts = torch.zeros(world, dtype=torch.int64, device=device)
         dist.all_gather_into_tensor(counts, n, group=group)

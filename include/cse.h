@@ -126,6 +126,36 @@ int cse_noise_estimate(int method, const double* P, int64_t n_sig, int T, int B,
                        cse_stream_t stream);
 
 /*
+ * Estimator constructor parameters (noise_estimation.py:12-13, :60) and the
+ * TrueNoise frame fit (:149-153), for cse_noise_estimate_ex.
+ * cse_noise_default_params() fills the reference's defaults.
+ */
+typedef struct cse_noise_params {
+    double percentile;       /* PercentileNoiseEstimator(percentile=20.0)             */
+    double max_fraction;     /*   max_fraction=0.30                                   */
+    double floor_rel;        /*   floor_rel=0.02                                      */
+    double smoothing_factor; /* MinTrackingNoiseEstimator(smoothing_factor=None): NaN = None */
+    int32_t min_frames;      /* PercentileNoiseEstimator min_frames=10                */
+    int32_t adaptive_short;  /*   adaptive_short=True                                 */
+    int32_t window_size;     /* MinTrackingNoiseEstimator(window_size=50)             */
+    int32_t src_frames;      /* CSE_NOISE_TRUE: frames of P (STFT of the trimmed noisy - clean);
+                                rows t >= src_frames repeat the last one (np.pad mode='edge'),
+                                src_frames > T is trimmed.  0 = T.  Ignored otherwise. */
+} cse_noise_params_t;        /* 48 bytes */
+
+void cse_noise_default_params(cse_noise_params_t* prm);
+
+/*
+ * cse_noise_estimate with estimator parameters (host struct, read at call
+ * time).  P is [n_sig][T][B] (CSE_NOISE_TRUE: [n_sig][src_frames][B]); N and
+ * the T < 5 fallback (:194-195) as for cse_noise_estimate.  Parameters a
+ * method does not read are ignored, as the reference's **kwargs swallow them.
+ */
+int cse_noise_estimate_ex(int method, const double* P, int64_t n_sig, int T, int B,
+                          const cse_noise_params_t* prm, double eps, float* N, void* workspace,
+                          cse_stream_t stream);
+
+/*
  * Time-varying noise PSD for the smoothed / frame-padded cases, fp64 math:
  *   src = N [n_sig][src_frames][B] with src_frames == T, or src_frames == 1: a
  *   static estimate that librosa.util.fix_length(..., size=T, axis=1)

@@ -87,7 +87,10 @@ def simple_noise(power, eps=1e-10):
 def noise_estimation(y, sr, method="percentile", n_fft=1024, hop_length=256,
                      win_length=None, estimator_params=None, window="hann",
                      center=True, pad_mode="reflect", **kwargs):
-    """Dispatch of noise_estimation.py:158-212 (kwargs reach the estimator)."""
+    """Dispatch of noise_estimation.py:158-212.  The estimator is constructed
+    from {**estimator_params, **kwargs} (:175, :197), estimate() reads eps and
+    clean_audio from **kwargs alone (:199-210); the T < 5 fallback reads eps
+    from the merged dict (:191-195)."""
     params = dict(estimator_params or {})
     params.update(kwargs)
     y = np.asarray(y, dtype=np.float64)
@@ -95,21 +98,20 @@ def noise_estimation(y, sr, method="percentile", n_fft=1024, hop_length=256,
         y = y.mean(axis=1)
     power = np.abs(stft(y, n_fft, hop_length, win_length, window, center,
                         pad_mode)) ** 2
-    eps = params.get("eps", 1e-10)
     if power.shape[1] < 5:
-        return simple_noise(power, eps)
+        return simple_noise(power, params.get("eps", 1e-10))
     if method == "percentile":
         keys = ("percentile", "min_frames", "max_fraction", "floor_rel",
                 "adaptive_short")
-        return percentile_noise(power, eps=eps,
+        return percentile_noise(power, eps=kwargs.get("eps", 1e-10),
                                 **{k: params[k] for k in keys if k in params})
     if method == "min_tracking":
         keys = ("window_size", "smoothing_factor")
-        return min_tracking_noise(power, eps=eps,
+        return min_tracking_noise(power, eps=kwargs.get("eps", 1e-10),
                                   **{k: params[k] for k in keys if k in params})
     if method == "true_noise":
-        return true_noise(power, y, params.get("clean_audio"), n_fft, hop_length,
-                          eps=params.get("eps", 1e-12))
+        return true_noise(power, y, kwargs.get("clean_audio"), n_fft, hop_length,
+                          eps=kwargs.get("eps", 1e-12))
     raise ValueError(f"Unbekannte Methode: {method}")
 
 

@@ -76,3 +76,21 @@ def rank_main(rank, world, port, outdir):
                  ids=np.array(calls[0] if calls else [], dtype=np.int64))
     finally:
         dist.destroy_process_group()
+
+
+def oracle_cell_full(args):
+    """One 10-s cell through the oracle for the full-size sweep test: the
+    enhanced waveform, finalize_enhanced's lag, the aligned SNR and STOI (of the
+    output rounded to f32, the type the device writes).  Pool worker."""
+    import oracle
+    from oracle import stoi_ref
+    from classical_speech_enhancement_amd.synth import make_pair
+    pair, alg, p, seconds = args
+    clean, noisy = make_pair(pair, seconds)
+    y = oracle.ALGORITHMS[alg](noisy, 16000, **p)
+    lag = oracle.align_lag(clean, y, 16000) or 0
+    e = oracle.finalize_enhanced(y, clean, 16000)
+    snr = oracle.calculate_snr(clean, e)
+    e32 = oracle.finalize_enhanced(np.asarray(y, np.float32).astype(np.float64), clean, 16000)
+    st = stoi_ref.calculate_stoi(clean, e32, 16000)
+    return y, int(lag), snr, np.nan if st is None else st

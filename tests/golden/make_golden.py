@@ -200,6 +200,49 @@ def gen_tiny(R):
     print("tiny done", sum(k.startswith("err|") for k in out), "errors")
 
 
+# estimator constructor parameters (noise_estimation.py:12-13, :60) exercised
+# through noise_estimation(estimator_params=..., **kwargs)
+NOISE_PARAM_CASES = [
+    ("percentile", dict(estimator_params=dict(min_frames=4, max_fraction=0.5, floor_rel=0.05),
+                        percentile=30.0)),
+    ("percentile", dict(estimator_params=dict(adaptive_short=False, floor_rel=0.0),
+                        percentile=10.0)),
+    ("percentile", dict(min_frames=40, max_fraction=0.1, percentile=20.0)),
+    ("percentile", dict(estimator_params=dict(eps=1e-3), percentile=20.0)),  # eps: kwargs only
+    ("min_tracking", dict(estimator_params=dict(window_size=20, smoothing_factor=0.7))),
+    ("min_tracking", dict(window_size=2, eps=1e-12)),
+    ("min_tracking", dict(estimator_params=dict(smoothing_factor=0.0, window_size=101))),
+]
+
+
+def gen_noise_params(R):
+    """Fixture 7: estimator parameters and a clean reference shorter than the
+    noisy signal (TrueNoise trim + frame edge-pad, noise_estimation.py:128-153),
+    through noise_estimation and through every algorithm."""
+    clean, noisy = make_pair(7, seconds=0.75)
+    _, short_noisy = make_pair(17, seconds=20 * 128 / 16000.0)  # T = 21 (< 30: adaptive_short)
+    out = {"clean": clean, "noisy": noisy, "short_noisy": short_noisy}
+    for i, (method, kw) in enumerate(NOISE_PARAM_CASES):
+        for tag, x in (("n", noisy), ("s", short_noisy)):
+            for n_fft, hop in ((512, 128), (1024, 256)):
+                N = R["noise"](x, sr=16000, method=method, n_fft=n_fft, hop_length=hop, **kw)
+                out[f"N|{i}|{tag}|{n_fft}|{hop}"] = np.asarray(N, dtype=np.float64)
+    for m in (len(clean) - 1000, 3000, 300):
+        c = clean[:m]
+        out[f"clean_len|{m}"] = np.asarray(m)
+        for n_fft, hop in ((512, 128), (1024, 256)):
+            N = R["noise"](noisy, sr=16000, method="true_noise", n_fft=n_fft, hop_length=hop,
+                           clean_audio=c, eps=1e-12)
+            out[f"Ntrue|{m}|{n_fft}|{hop}"] = np.asarray(N, dtype=np.float64)
+            for alg, base in CELLS.items():
+                y = R[alg](noisy, 16000, **dict(base, n_fft=n_fft, hop_length=hop,
+                                                noise_percentile=10.0, noise_method="true_noise",
+                                                clean_audio=c))
+                out[f"y|{m}|{alg}|{n_fft}|{hop}"] = np.asarray(y, dtype=np.float64)
+    np.savez_compressed(os.path.join(OUT, "noise_params.npz"), **out)
+    print("noise_params done", len(out))
+
+
 def _read_wav(path):
     with wave.open(path) as w:
         assert w.getsampwidth() == 2 and w.getnchannels() == 1
@@ -252,7 +295,8 @@ def gen_presentation(R):
 
 if __name__ == "__main__":
     R = ref_modules()
-    which = sys.argv[1:] or ["algorithms", "config1", "short", "presentation", "grid", "tiny"]
+    which = sys.argv[1:] or ["algorithms", "config1", "short", "presentation", "grid", "tiny",
+                             "noise_params"]
     if "algorithms" in which:
         gen_algorithms(R)
     if "config1" in which:
@@ -265,3 +309,5 @@ if __name__ == "__main__":
         gen_grid_snr(R)
     if "tiny" in which:
         gen_tiny(R)
+    if "noise_params" in which:
+        gen_noise_params(R)

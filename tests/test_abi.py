@@ -34,7 +34,7 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_version_and_error_channel(lib):
-    assert lib.cse_version() == 3
+    assert lib.cse_version() == _lib.ABI_VERSION
     rc = lib.cse_stft(None, None, 1, 100, 512, 128, None, None, None)
     assert rc == -1
     assert b"x is NULL" in lib.cse_last_error()

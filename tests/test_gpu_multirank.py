@@ -47,9 +47,9 @@ def test_bench_two_ranks_weak_scaling(gpu):
     assert len(lines) == 1, out.stdout  # rank 0 prints the one line
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
-    units = d["config"]["units_per_step_per_gpu"]
-    assert d["value"] == pytest.approx(2 * units * d["steps"] / (d["ms_per_step"] * d["steps"] / 1e3),
-                                       rel=1e-6)
+    units = d["config"]["units_per_step"]  # both ranks' pairs
+    assert units == 2 * d["config"]["units_per_step_rank0"]
+    assert d["value"] == pytest.approx(units / (d["ms_per_step"] / 1e3), rel=1e-6)
 
 
 def _rank(rank, world, port, outdir):
@@ -83,4 +83,73 @@ def test_run_grid_two_ranks_equals_one_process(gpu, tmp_path):
     specs = search.job_specs(len(noisy), grids=SMALL_GRIDS)
     ref, _ = search.run_grid(clean, noisy, specs)
     assert np.array_equal(t0, t1, equal_nan=True)
+    assert np.array_equal(t0, ref, equal_nan=True)
+
+
+def test_bench_two_ranks_strong_scaling(gpu):
+    """--pairs-total: the fixed job's cells split by search.assign_lpt; value
+    counts the whole job once."""
+    env = dict(os.environ, CSE_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--pairs-total", "3", "--seconds", "2", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    units = d["config"]["units_per_step"]
+    assert d["value"] == pytest.approx(units / (d["ms_per_step"] / 1e3), rel=1e-6)
+    assert 0 < d["config"]["units_per_step_rank0"] < units
+
+
+def test_bench_rccl_world1(gpu):
+    """bench.py under torchrun with the default backend "nccl" (RCCL) at world
+    size 1: the per-step all_gather_into_tensor of device records, the
+    all_reduce of the step time and the barriers run through RCCL."""
+    env = {k: v for k, v in os.environ.items() if k != "CSE_DIST_BACKEND"}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
+           "--pairs-total", "2", "--seconds", "2", "--no-cpu-baseline", "--no-parity"]
+    out = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert d["n_gpus"] == 1 and "RCCL" in d["config"]["parallelism"]
+
+
+def _rccl_rank(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from classical_speech_enhancement_amd import search
+    from _grid_worker import SMALL_GRIDS, pairs
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world)
+    try:
+        assert dist.get_backend() == "nccl"
+        clean, noisy = pairs(3, 1.2)
+        specs = search.job_specs(len(noisy), grids=SMALL_GRIDS)
+        table, _ = search.run_grid(clean, noisy, specs)  # device=None -> this rank's GPU
+        np.save(os.path.join(outdir, f"rccl{rank}.npy"), table)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_run_grid_rccl_world1_equals_local(gpu, tmp_path):
+    """search.run_grid / gather_records under init_process_group("nccl"): the
+    count and record all_gather_into_tensor calls move device tensors through
+    RCCL; the table equals the one computed without torch.distributed."""
+    import torch.multiprocessing as tmp
+    from classical_speech_enhancement_amd import search
+    from _grid_worker import SMALL_GRIDS, pairs
+    tmp.spawn(_rccl_rank, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
+    t0 = np.load(tmp_path / "rccl0.npy")
+    clean, noisy = pairs(3, 1.2)
+    specs = search.job_specs(len(noisy), grids=SMALL_GRIDS)
+    ref, _ = search.run_grid(clean, noisy, specs)
     assert np.array_equal(t0, ref, equal_nan=True)

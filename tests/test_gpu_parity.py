@@ -339,3 +339,39 @@ def test_long_signal_beyond_8192_frames(P):
     with pytest.raises(CseError):
         P.advanced_mmse(long, 16000, **dict(CELLS["omlsa"], n_fft=512, hop_length=128,
                                             noise_percentile=10.0, noise_method="percentile"))
+
+
+def test_noise_params_and_short_clean_match_reference_golden(P):
+    """Estimator constructor parameters through plugins.noise_estimation, and a
+    clean reference shorter than the noisy signal (TrueNoise trim + frame
+    edge-pad, noise_estimation.py:128-153) through noise_estimation and every
+    algorithm plugin, against the reference's outputs."""
+    from test_oracle_golden import _noise_param_cases
+    g = load_golden("noise_params.npz")
+    xs = {"n": g["noisy"], "s": g["short_noisy"]}
+    for i, (method, kw) in enumerate(_noise_param_cases()):
+        for tag, x in xs.items():
+            for n_fft, hop in ((512, 128), (1024, 256)):
+                N = P.noise_estimation(x, 16000, method=method, n_fft=n_fft, hop_length=hop,
+                                       **kw)
+                ref = g[f"N|{i}|{tag}|{n_fft}|{hop}"]
+                assert N.shape == ref.shape, (i, tag)
+                np.testing.assert_allclose(N, ref, rtol=1e-6, atol=0, err_msg=f"{i}|{tag}")
+    clean, noisy = g["clean"], g["noisy"]
+    n = 0
+    for key in g.files:
+        if key.startswith("Ntrue|"):
+            m, n_fft, hop = map(int, key.split("|")[1:])
+            N = P.noise_estimation(noisy, 16000, method="true_noise", n_fft=n_fft,
+                                   hop_length=hop, clean_audio=clean[:m], eps=1e-12)
+            assert N.shape == g[key].shape
+            np.testing.assert_allclose(N, g[key], rtol=1e-6, atol=0, err_msg=key)
+        elif key.startswith("y|"):
+            m, alg, n_fft, hop = key.split("|")[1:]
+            y = _fn(P, alg)(noisy, 16000, **dict(CELLS[alg], n_fft=int(n_fft),
+                                                 hop_length=int(hop), noise_percentile=10.0,
+                                                 noise_method="true_noise",
+                                                 clean_audio=clean[:int(m)]))
+            assert rel_l2(y, g[key]) <= TOL and rel_max(y, g[key]) <= TOL, key
+            n += 1
+    assert n == 24

@@ -32,7 +32,8 @@ def test_run_sweep_files_and_selection(tmp_path):
         pair = stems.index(r["stem"])
         cid, score = best[(pair, r["alg"])]
         # the device pick scores within float noise of the oracle's pick
-        assert abs(r["snr_balopt"] - score) < 1e-3, r
+        assert abs(r["snr_snropt"] - score) < 1e-3, r
+        assert r["snr_balopt"] is None and r["best_params_balanced"] == {}
         sid, sscore = best_stoi[(pair, r["alg"])]
         assert abs(r["stoi_stoiopt"] - sscore) < 4e-6, r
         assert abs(r["stoi_noisy"] - stoi_ref.stoi(clean[pair], noisy[pair].astype(np.float32)

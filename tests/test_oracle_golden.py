@@ -161,3 +161,42 @@ def test_stft_istft_roundtrip(n):
         assert Y.shape == (n_fft // 2 + 1, 1 + n // hop)
         y = oracle.istft(Y, hop_length=hop, length=n)
         assert rel_l2(y, x) < 1e-12
+
+
+def _noise_param_cases():
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "make_golden", os.path.join(os.path.dirname(__file__), "golden", "make_golden.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)  # defines data only; the reference is imported in main
+    return mod.NOISE_PARAM_CASES
+
+
+def test_noise_params_and_short_clean_match_reference():
+    """Estimator constructor parameters (noise_estimation.py:12-13, :60) and a
+    clean reference shorter than the noisy signal (TrueNoise trim + edge-pad,
+    :128-153) against the reference's own outputs."""
+    g = load_golden("noise_params.npz")
+    xs = {"n": g["noisy"], "s": g["short_noisy"]}
+    for i, (method, kw) in enumerate(_noise_param_cases()):
+        for tag, x in xs.items():
+            for n_fft, hop in ((512, 128), (1024, 256)):
+                N = oracle.noise_estimation(x, 16000, method=method, n_fft=n_fft,
+                                            hop_length=hop, **kw)
+                ref = g[f"N|{i}|{tag}|{n_fft}|{hop}"]
+                assert N.shape == ref.shape
+                assert rel_max(N, ref) < 1e-12, (i, tag, n_fft)
+    clean, noisy = g["clean"], g["noisy"]
+    for key in g.files:
+        if key.startswith("Ntrue|"):
+            m, n_fft, hop = map(int, key.split("|")[1:])
+            N = oracle.noise_estimation(noisy, 16000, method="true_noise", n_fft=n_fft,
+                                        hop_length=hop, clean_audio=clean[:m], eps=1e-12)
+            assert rel_max(N, g[key]) < 1e-12, key
+        elif key.startswith("y|"):
+            m, alg, n_fft, hop = key.split("|")[1:]
+            y = ALG[alg](noisy, 16000, **dict(CELLS[alg], n_fft=int(n_fft), hop_length=int(hop),
+                                              noise_percentile=10.0, noise_method="true_noise",
+                                              clean_audio=clean[:int(m)]))
+            assert rel_max(y, g[key]) < 1e-12, key

@@ -14,7 +14,25 @@ def test_row_has_every_reference_key():
     for k in results.ROW_KEYS:
         assert k in row
     assert row["stoi_noisy"] is None and row["pesq_balopt"] is None
-    assert row["snr_balopt"] == 7.5 and row["best_params_snr"] == {"alpha": 0.98}
+    assert row["snr_snropt"] == 7.5 and row["best_params_snr"] == {"alpha": 0.98}
+
+
+def test_reference_keys_keep_reference_meaning():
+    """run_algorithm_on_pair (speech_enhancement_comparison.py:314-338): *_stoiopt
+    are the STOI-optimal cell's scores, *_pesqopt the PESQ-optimal cell's,
+    *_balopt the balance-optimal cell's (balance = STOI and PESQ, :104-115).
+    Without PESQ only the STOI objective is scored: the PESQ and balance
+    columns stay None / {}; the SNR-optimal cell lives under its own keys."""
+    row = results.result_row("p01", "omlsa", 16000, 3.2, 9.1, {"q": 0.5}, stoi_noisy=0.71,
+                             stoi_best=0.83, stoi_params={"q": 0.3}, snr_stoiopt=8.4)
+    assert row["stoi_noisy"] == 0.71 and row["snr_noisy"] == 3.2
+    assert row["stoi_stoiopt"] == 0.83 and row["snr_stoiopt"] == 8.4
+    assert row["best_params_stoi"] == {"q": 0.3}
+    for k in ("pesq_noisy", "pesq_stoiopt", "stoi_pesqopt", "pesq_pesqopt", "snr_pesqopt",
+              "stoi_balopt", "pesq_balopt", "snr_balopt"):
+        assert row[k] is None, k
+    assert row["best_params_pesq"] == {} and row["best_params_balanced"] == {}
+    assert row["snr_snropt"] == 9.1 and row["best_params_snr"] == {"q": 0.5}
 
 
 def test_summary_csv_and_json(tmp_path):
@@ -22,13 +40,14 @@ def test_summary_csv_and_json(tmp_path):
             results.result_row("b", "mmse", 16000, 2.0, 7.0, {}),
             results.result_row("a", "wiener", 16000, 1.0, 4.0, {})]
     summary = results.write_summary(rows, ["mmse", "wiener", "omlsa"], str(tmp_path))
-    assert summary["mmse"]["count"] == 2 and summary["mmse"]["snr_balopt_mean"] == 6.0
-    assert summary["omlsa"]["count"] == 0 and summary["omlsa"]["snr_balopt_mean"] is None
+    assert summary["mmse"]["count"] == 2 and summary["mmse"]["snr_snropt_mean"] == 6.0
+    assert summary["mmse"]["snr_balopt_mean"] is None
+    assert summary["omlsa"]["count"] == 0 and summary["omlsa"]["snr_snropt_mean"] is None
     assert summary["mmse"]["stoi_noisy_mean"] is None
     lines = (tmp_path / "all_results.csv").read_text().splitlines()
     assert lines[0] == ("stem,alg,stoi_noisy,pesq_noisy,stoi_stoiopt,pesq_stoiopt,stoi_pesqopt,"
                         "pesq_pesqopt,stoi_balopt,pesq_balopt,snr_balopt")
-    assert lines[1] == "a,mmse,NA,NA,NA,NA,NA,NA,NA,NA,5.0000"
+    assert lines[1] == "a,mmse,NA,NA,NA,NA,NA,NA,NA,NA,NA"
     back = json.loads((tmp_path / "all_results.json").read_text())
     assert back[2]["alg"] == "wiener"
     assert json.loads((tmp_path / "summary_means.json").read_text())["wiener"]["count"] == 1
