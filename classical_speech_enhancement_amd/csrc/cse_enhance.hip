@@ -14,8 +14,9 @@
 // L = M/16 lanes own one cell (16 lanes @512, 32 @1024), so a wave carries
 // CPW = 64/L cells.  Each lane holds 16 bins (+ the Nyquist bin on lane 0):
 // the serial-in-t recursion state lives in registers, the frames stream
-// through.  Per frame the cell's 257/513 complex bins go through LDS twice
-// (mirror pairing for the real-IFFT packing, one 16 x L transpose); the
+// through.  Per frame the cell's bins pass through a half-spectrum LDS buffer
+// twice (mirror pairing for the real-IFFT packing, own bins stay in registers)
+// and a half transpose block twice (16 x L transpose in two 8-row rounds); the
 // two length-16 DFT passes run in registers.  The inverse FFT's outputs land
 // on lanes so that every lane owns output samples with fixed residues mod 32
 // (mod 64 @1024): the overlap-add accumulator never leaves registers, and
@@ -33,10 +34,6 @@ struct Geo {
     static constexpr int L = M / 16;          // lanes per cell
     static constexpr int CPW = 64 / L;        // cells per wave
     static constexpr int SP = NFFT / 16;      // spacing of a lane's output samples
-    static constexpr int SROW = M + 16;       // S row stride (complex), bank-shifted
-    static constexpr int TROW = L + 1;        // transpose row stride (complex)
-    static constexpr int TCELL = 16 * TROW;   // transpose block per cell
-    static constexpr int REGION = (CPW * SROW > CPW * TCELL) ? CPW * SROW : CPW * TCELL;
 };
 
 struct Args {
@@ -53,59 +50,21 @@ struct Args {
     uint8_t* finite;
 };
 
-// ---------------------------------------------------------------------------
-// special functions (fp32), coefficients from tools/gen_special.py
-// ---------------------------------------------------------------------------
-// Estrin's scheme: E(c[lo, lo+n)) = E(c[lo, lo+h)) + t^h E(c[lo+h, lo+n)), h the
-// largest power of two < n.  Depth ~log2(n) instead of Horner's n dependent
-// FMAs (the gain chains are latency-bound at 3 waves/SIMD); tools/gen_special.py
-// checks exactly this evaluation order in fp32.
-template <int LO, int N, int K, int NP>
-__device__ __forceinline__ float estrin_rec(const float (&c)[K], const float (&pw)[NP]) {
-    if constexpr (N == 1) {
-        return c[LO];
-    } else if constexpr (N == 2) {
-        return fmaf(c[LO + 1], pw[0], c[LO]);
-    } else {
-        constexpr int LH = 31 - __builtin_clz(N - 1);  // log2 of the largest power of two < N
-        constexpr int H = 1 << LH;
-        return fmaf(estrin_rec<LO + H, N - H>(c, pw), pw[LH], estrin_rec<LO, H>(c, pw));
-    }
-}
-
 #ifdef CSE_MARKS  // static instruction-count analysis builds only (tools/isa_sections.py)
 #define CSE_MARK(name) asm volatile(";#MARK " name)
 #else
 #define CSE_MARK(name)
 #endif
-// CSE_PRIO: bit 1 raises the wave's issue priority (s_setprio) over the gain
-// stage, so a wave in its VALU-dense stage is issued ahead of waves in their
-// LDS-bound IFFT/retire stages, whose latency then overlaps it
-// (13 pairs: 33.3 -> 31.5 ms).  Bits 2 and 4 (priority over the IFFT passes)
-// measured slower.
-#ifndef CSE_PRIO
-#define CSE_PRIO 1
-#endif
-#ifndef CSE_PRIO_LEVEL
-#define CSE_PRIO_LEVEL 1
-#endif
-#ifndef CSE_ESTRIN
-#define CSE_ESTRIN 0
-#endif
+
+// ---------------------------------------------------------------------------
+// special functions (fp32), coefficients from tools/gen_special.py
+// ---------------------------------------------------------------------------
 template <int N>
 __device__ __forceinline__ float horner(const float (&c)[N], float t) {
-    if constexpr (!CSE_ESTRIN) {
-        float acc = c[N - 1];
+    float acc = c[N - 1];
 #pragma unroll
-        for (int k = N - 2; k >= 0; --k) acc = fmaf(acc, t, c[k]);
-        return acc;
-    }
-    constexpr int NP = 32 - __builtin_clz(N - 1);  // powers t, t^2, ..., t^(2^(NP-1))
-    float pw[NP];
-    pw[0] = t;
-#pragma unroll
-    for (int k = 1; k < NP; ++k) pw[k] = pw[k - 1] * pw[k - 1];
-    return estrin_rec<0, N>(c, pw);
+    for (int k = N - 2; k >= 0; --k) acc = fmaf(acc, t, c[k]);
+    return acc;
 }
 
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
@@ -113,7 +72,6 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 __device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }
 
 constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kLn2 = 0.6931471805599453f;
 
 // exp(-v/2)[(1+v)I0(v/2) + v I1(v/2)] for v in [1e-12, 80]
 __device__ __forceinline__ float mmse_bracket(float v, float sqrtv) {
@@ -127,19 +85,19 @@ __device__ __forceinline__ float mmse_bracket(float v, float sqrtv) {
 }
 
 // ---------------------------------------------------------------------------
-// per-bin gains.  P = |Y|^2; inv = 1/max(N, eps) prepared per noise row by the
-// host-side pipeline (cse_noise_invert), so gamma = max(P*inv, eps) exactly as
-// max(P/max(N,eps), eps) up to one rounding.  The decision-directed recursion
-// only ever uses prev_gain**2 * prev_gamma (wiener_filter.py:133, mmse.py:82,
+// per-bin gains.  The a-posteriori SNR gamma = max(P/max(N, eps), eps) depends
+// only on the frame's spectrum row and noise row, which every cell of a
+// workgroup shares: the row stager computes it once per bin and frame
+// (P * inv with inv = 1/max(N, eps) from cse_noise_invert), and the cells read
+// it from LDS.  The decision-directed recursion only ever uses
+// prev_gain**2 * prev_gamma (wiener_filter.py:133, mmse.py:82,
 // advanced_mmse.py:215): the carried state is rr = (G*G)*gamma.
 // ---------------------------------------------------------------------------
 // First frame: the reference uses xi = d (Wiener) / max(gamma-1, ksi_min)
 // (MMSE, OMLSA); with rr = 0 and alpha_t = 0 on frame 0 the general DD
 // expression alpha_t*rr + (1-alpha_t)*max(gamma-1, 0) gives exactly that (for
 // ksi_min >= 0), so there is no per-bin branch to split the scheduling region.
-__device__ __forceinline__ float gain_wiener(float P, float inv, float& rr, float alpha_t,
-                                             float gfloor) {
-    const float gam = fmaxf(P * inv, 1e-10f);
+__device__ __forceinline__ float gain_wiener(float gam, float& rr, float alpha_t, float gfloor) {
     const float d = fmaxf(gam - 1.0f, 0.0f);
     const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * d, 1e-10f);
     const float g = fminf(fmaxf(xi * fast_rcp(1.0f + xi), gfloor), 1.0f);
@@ -147,9 +105,8 @@ __device__ __forceinline__ float gain_wiener(float P, float inv, float& rr, floa
     return g;
 }
 
-__device__ __forceinline__ float gain_mmse(float P, float inv, float& rr, float alpha_t,
-                                           float ksi_min, float gmin, float gmax) {
-    const float gam = fmaxf(P * inv, 1e-12f);
+__device__ __forceinline__ float gain_mmse(float gam, float& rr, float alpha_t, float ksi_min,
+                                           float gmin, float gmax) {
     const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * fmaxf(gam - 1.0f, 0.0f), ksi_min);
     const float v = __builtin_amdgcn_fmed3f(xi * gam * fast_rcp(1.0f + xi), 1e-12f, 80.0f);
     const float sv = __builtin_amdgcn_sqrtf(v);
@@ -173,10 +130,8 @@ __device__ __forceinline__ float gain_mmse(float P, float inv, float& rr, float 
 // 0 <= X <= 1e6, so lg is finite or -inf (xi = 0 with ksi_min = 0), and -inf
 // gives g = exp2(-inf) = 0 -> clip -> gain_floor, the reference's 0**p * gf**(1-p)
 // clipped (p >= 1e-10 > 0).  Non-finite input makes the cell non-finite either way.
-__device__ __forceinline__ float gain_omlsa(float P, float inv, float& rr, float alpha_t,
-                                            float ksi_min, float gfloor, float lg2_floor, float q,
-                                            float vmax) {
-    const float gam = fmaxf(P * inv, 1e-10f);
+__device__ __forceinline__ float gain_omlsa(float gam, float& rr, float alpha_t, float ksi_min,
+                                            float gfloor, float lg2_floor, float q, float vmax) {
     const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * fmaxf(gam - 1.0f, 0.0f), ksi_min);
     const float r = fast_rcp(1.0f + xi);
     const float xr = xi * r;
@@ -196,60 +151,28 @@ __device__ __forceinline__ float gain_omlsa(float P, float inv, float& rr, float
 // ---------------------------------------------------------------------------
 // Block -> slot-group order.  Blocks are dealt round-robin over the 8 XCDs
 // (block b runs on XCD b % 8, as its (b/8)-th block there), and the host sorts
-// slot groups longest-first with groups that share rows adjacent.
-//   CSE_XCD_MAP 0: identity (XCDs interleave group by group)
-//   CSE_XCD_MAP 1: each XCD a contiguous slice (best L2 reuse, but XCD 0 gets
-//                  all the longest groups)
-//   CSE_XCD_MAP 2: runs of CSE_XCD_RUN consecutive groups per XCD, the runs
-//                  dealt round-robin: L2 reuse inside a run, balanced XCDs
+// slot groups longest-first with groups that share rows adjacent.  Runs of
+// RUN consecutive groups go to one XCD (L2 reuse of the shared Y/N rows inside
+// a run) and the runs are dealt round-robin, which keeps the XCDs balanced
+// (one contiguous slice per XCD gave XCD 0 all the longest groups:
+// 46.7 -> 33.3 ms at 13 pairs, r01).  The tail that does not fill 8 runs keeps
+// the identity order.
 // ---------------------------------------------------------------------------
-#ifndef CSE_XCD_MAP
-#define CSE_XCD_MAP 2
-#endif
-#ifndef CSE_XCD_RUN
-#define CSE_XCD_RUN 4
-#endif
 __device__ __forceinline__ int xcd_remap(int b, int nb) {
-    if (CSE_XCD_MAP == 0) return b;
+    constexpr int RUN = 4;
     const int xcd = b % 8, idx = b / 8;
-    if (CSE_XCD_MAP == 1) {
-        const int q = nb / 8, r = nb % 8;
-        return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-    }
-    // runs: chunk k (k = idx / RUN) of XCD x covers groups [(k*8 + x)*RUN, +RUN)
-    constexpr int RUN = CSE_XCD_RUN;
     const int g = ((idx / RUN) * 8 + xcd) * RUN + idx % RUN;
-    // the tail (nb not a multiple of 8*RUN) falls back to the identity order
     const int full = (nb / (8 * RUN)) * (8 * RUN);
     return b < full ? g : b;
 }
 
 // ---------------------------------------------------------------------------
-// Workgroup = 3 waves = CPWG cells that share hop, algorithm, spectrum Y,
-// noise row and clean reference (the host packs them so).  Per frame the
-// workgroup stages the shared rows (Y[t][:], N[t][:], clean[retired samples])
-// into LDS once, cooperatively, one frame ahead (a few VGPRs per thread),
-// instead of every lane keeping 17 bins of loads in flight.
+// Workgroup = CSE_WG_WAVES waves = CPWG cells that share hop, algorithm,
+// spectrum Y, noise row and clean reference (the host packs them so).  Per
+// frame the workgroup stages the shared rows (Y[t][:], gamma[t][:] (N[t][:] for
+// SS), clean[retired samples]) into LDS once, cooperatively, one frame ahead
+// (a few VGPRs per thread).
 // ---------------------------------------------------------------------------
-// CSE_DIRECT_ROWS=1: every lane loads its own Y/N bins from global memory
-// (L1/L2-resident: the 12 cells of a workgroup read the same rows) one frame
-// ahead into registers, and each wave stages its own clean row in LDS, so the
-// frame loop has no workgroup barrier.  0: the workgroup stages shared Y/N/C
-// rows in LDS, one barrier per frame.
-#ifndef CSE_DIRECT_ROWS
-#define CSE_DIRECT_ROWS 0  // r01: 1 measured equal (31.3 vs 31.0 ms at 8 pairs, 92 B spill)
-#endif
-// where the next frame's Y/N loads are issued: 0 after the gain stage,
-// 1 after the transpose, 2 before the retire
-#ifndef CSE_PREFETCH_AT
-#define CSE_PREFETCH_AT 0
-#endif
-
-// CSE_LDS_PAD: extra LDS bytes per workgroup (occupancy experiments only)
-#ifndef CSE_LDS_PAD
-#define CSE_LDS_PAD 0
-#endif
-
 template <int NFFT>
 struct WG {
     using G = Geo<NFFT>;
@@ -257,28 +180,33 @@ struct WG {
     static constexpr int THREADS = 64 * WAVES;
     static constexpr int CPWG = WAVES * G::CPW;                   // cells per workgroup
     static constexpr int HMAX = 256;                              // largest hop
-    static constexpr int TR = G::L + 1;                           // padded transpose row
-    // per-cell LDS region: S row (B complex) aliased with the 16 x (L+1)
-    // transpose block.  16*17*8 = 2176 B = 128 mod 256: the two cells of a
-    // 32-lane group read disjoint bank halves in the transposed read.
-    static constexpr int CREG_RAW = (G::B * 8 > 16 * TR * 8) ? G::B * 8 : 16 * TR * 8;
-    static constexpr int CREG = ((CREG_RAW + 127) / 128) * 128 + (((CREG_RAW + 127) / 128) % 2 ? 0 : 128);
-    static constexpr int OFF_CELLS = 0;
+    // per-cell LDS region: the mirror-exchange slots (9 complex per lane,
+    // stride 72 B: the 16 lanes of a ds_write_b64 group hit disjoint banks)
+    // aliased with the half transpose block (16 x 9 / 18 complex).  Its size is an
+    // odd multiple of 128 B, so the two cells of a 32-lane ds_read_b64 group
+    // (n_fft 512) sit in disjoint bank halves of the transposed reads.
+    static constexpr int XB = G::L * 9 * 8;
+    static constexpr int TB = 16 * ((G::L == 16) ? 9 : 18) * 8;
+    static constexpr int CREG_RAW = XB > TB ? XB : TB;
+    static constexpr int CREG_U = (CREG_RAW + 127) / 128;
+    static constexpr int CREG = (CREG_U + (CREG_U % 2 ? 0 : 1)) * 128;
     static constexpr int YROW = ((G::B * 8 + 15) / 16) * 16;      // bytes of one Y row
-    static constexpr int NROW = ((G::B * 4 + 15) / 16) * 16;      // bytes of one N row
+    static constexpr int GROW = ((G::B * 4 + 15) / 16) * 16;      // bytes of one gamma / N row
     static constexpr int OFF_Y = CPWG * CREG;                     // float2[2][B] (double buffer)
-    static constexpr int OFF_N = OFF_Y + (CSE_DIRECT_ROWS ? 0 : 2 * YROW);  // float[2][B]
-    static constexpr int OFF_C = OFF_N + (CSE_DIRECT_ROWS ? 0 : 2 * NROW);  // float[(waves)][2][HMAX]
-    static constexpr int CBUF = 2 * HMAX * 4;                     // one clean double buffer
-    // n_fft 1024 fits 3 workgroups per CU (12 waves instead of 8) by halving
-    // two tables: the pass-1 twiddles keep the 16 lane residues b2, since
-    // e^{2πi (b2 + 16 h2) b/M} = tw[b][b2] W32^{h2 b}; the window keeps slots
-    // q < 16, since slot q + 16 is n + N/2 and w(n + N/2) = 1 - w(n)
+    static constexpr int OFF_G = OFF_Y + 2 * YROW;                // float[2][B]
+    static constexpr int OFF_C = OFF_G + 2 * GROW;                // float[2][HMAX]
+    static constexpr int CBUF = 2 * HMAX * 4;
+    // n_fft 1024 halves two tables: the pass-1 twiddles keep the 16 lane
+    // residues b2, since e^{2πi (b2 + 16 h2) b/M} = tw[b][b2] W32^{h2 b}; the
+    // window keeps slots q < 16, since slot q + 16 is n + N/2 and
+    // w(n + N/2) = 1 - w(n)
     static constexpr bool HALF_TABLES = (NFFT == 1024);
     static constexpr int TWL = HALF_TABLES ? 16 : G::L;          // twiddle columns
-    static constexpr int OFF_TW = OFF_C + (CSE_DIRECT_ROWS ? WAVES : 1) * CBUF;  // cf[15][TWL]
-    static constexpr int OFF_LC = OFF_TW + 15 * TWL * 8;          // cf[L] packing rotor
-    static constexpr int OFF_CP = OFF_LC + G::L * 8;              // float[CPWG][8] cell params
+    // pass-1 twiddles: one row of 18 complex (144 B) per column, entry b - 1:
+    // the ds_read_b128 of a 16-lane group hit disjoint banks
+    static constexpr int OFF_TW = OFF_C + CBUF;                   // cf[TWL][18]
+    static constexpr int OFF_LC = OFF_TW + TWL * 144;             // cf[L] packing rotor
+    static constexpr int OFF_CP = OFF_LC + G::L * 8;              // float[CPWG][8]
     // synthesis window w(n)/NFFT at the lane's 32 (16) sample slots; row stride
     // 36 (20) floats: the lanes of a ds_read_b128 group hit disjoint banks
     static constexpr int WSLOTS = HALF_TABLES ? 16 : 32;
@@ -288,26 +216,15 @@ struct WG {
     // (512/256), whose wss is not constant; row stride 20 floats (disjoint banks)
     static constexpr int ISTR = 20;
     static constexpr int OFF_IWS = OFF_WIN + G::L * WSTR * 4;
-    static constexpr int BYTES = OFF_IWS + (NFFT == 512 ? G::L * ISTR * 4 : 0) + CSE_LDS_PAD;
+    static constexpr int BYTES = OFF_IWS + (NFFT == 512 ? G::L * ISTR * 4 : 0);
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
-// LDS decides how many workgroups share a CU: keep >= 12 waves (3 per SIMD)
-static_assert(CSE_LDS_PAD || (163840 / WG<512>::BYTES) * CSE_WG_WAVES >= 12,
-              "n_fft=512 workgroups must fill 12 waves per CU");
-static_assert(CSE_LDS_PAD || (163840 / WG<1024>::BYTES) * CSE_WG_WAVES >= 12,
-              "n_fft=1024 workgroups must fill 12 waves per CU");
+// 4 workgroups (16 waves) per CU fit the LDS; the register budget then sets occupancy
+static_assert(4 * WG<512>::BYTES <= 163840, "n_fft=512 workgroups must fit 4 per CU");
+static_assert(4 * WG<1024>::BYTES <= 163840, "n_fft=1024 workgroups must fit 4 per CU");
 static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
               WG<1024>::CPWG == CSE_CELLS_PER_GROUP(1024), "cse.h slot-group size");
-
-// CSE_ABLATE (timing experiments only; 0 in every product build):
-//   1 = trivial gain (S = Y), 2 = no inverse FFT passes, 4 = no sample retire,
-//   8 = no workgroup barrier, 64 = no row staging, 128 = no LDS transpose
-//   (r01, 8 pairs: full 31.0 ms; 1 -> 19.0, 2 -> 26.7, 4 -> 30.4, 8 -> 28.6,
-//    15 -> 16.4, 15|64 -> 15.4, 15|128 -> 13.0, 15|64|128 -> 11.7)
-#ifndef CSE_ABLATE
-#define CSE_ABLATE 0
-#endif
 
 // waves per SIMD the register allocation targets (VGPR budget 512 / w)
 #ifndef CSE_WAVES_PER_SIMD
@@ -331,27 +248,16 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// window w(n)/NFFT at the lane's slot q (a compile-time index after unrolling)
-template <typename W>
-__device__ __forceinline__ float win_at(const float* wt, int q) {
-    if (W::HALF_TABLES && q >= 16) return (1.0f / (float)W::G::M / 2.0f) - wt[q - 16];
-    return wt[q];
-}
-
 // per-cell parameters as the gain stage wants them
 struct CellParam {
     float p0, p1, p2, p3, p4, lg2_floor, q_spp, pad;
 };
 static_assert(sizeof(CellParam) == 32, "CellParam layout");
 
+// One bin: gv is gamma (Wiener/MMSE/OMLSA) or the noise PSD N (SS).
 template <int ALGO>
-__device__ __forceinline__ cf gain_bin(float2 y, float nz, float& rr, float alpha_t,
+__device__ __forceinline__ cf gain_bin(float2 y, float gv, float& rr, float alpha_t,
                                        const CellParam& cp, float& g) {
-    const float P = y.x * y.x + y.y * y.y;
-    if (CSE_ABLATE & 1) {
-        g = nz;
-        return cmk(y.x * nz, y.y * nz);
-    }
     if (ALGO == CSE_ALGO_SS) {
         // Ps = max(P - a N, b N); |S| = sqrt(Ps) with the noisy phase
         // (spectral_subtractor.py:44-53).  No eps floor: the reference floors
@@ -360,7 +266,8 @@ __device__ __forceinline__ cf gain_bin(float2 y, float nz, float& rr, float alph
         // clip (fix_length zero-pads N, so Ps = P) reaches them: sqrt is
         // taken of a rescaled Ps below 2^-96, and the noisy phase y/|y| of a
         // rescaled y below 2^-50.
-        const float ps = fmaxf(P - cp.p0 * nz, cp.p1 * nz);
+        const float P = y.x * y.x + y.y * y.y;
+        const float ps = fmaxf(P - cp.p0 * gv, cp.p1 * gv);
         const bool tiny_ps = ps < 0x1p-96f;
         const float sp = __builtin_amdgcn_sqrtf(tiny_ps ? ps * 0x1p64f : ps) *
                          (tiny_ps ? 0x1p-32f : 1.0f);
@@ -372,63 +279,87 @@ __device__ __forceinline__ cf gain_bin(float2 y, float nz, float& rr, float alph
         return (pz > 0.0f) ? cmk(yx * u, yy * u) : cmk(sp, 0.0f);  // angle(0) = 0
     }
     if (ALGO == CSE_ALGO_WIENER)
-        g = gain_wiener(P, nz, rr, alpha_t, cp.p1);
+        g = gain_wiener(gv, rr, alpha_t, cp.p1);
     else if (ALGO == CSE_ALGO_MMSE)
-        g = gain_mmse(P, nz, rr, alpha_t, cp.p1, cp.p2, cp.p3);
+        g = gain_mmse(gv, rr, alpha_t, cp.p1, cp.p2, cp.p3);
     else
-        g = gain_omlsa(P, nz, rr, alpha_t, cp.p1, cp.p2, cp.lg2_floor, cp.q_spp, cp.p4);
+        g = gain_omlsa(gv, rr, alpha_t, cp.p1, cp.p2, cp.lg2_floor, cp.q_spp, cp.p4);
     return cmk(y.x * g, y.y * g);
 }
 
-// One frame's gain stage for one lane: bins i + L*j (j < 16) and, on lane 0,
-// the Nyquist bin M.  The row pointers are __restrict__ (the Y/N rows and the
-// cell's S row are disjoint LDS ranges), so after inlining the scheduler may
-// issue all 17 bins' reads up front and interleave the 17 independent gain
-// chains instead of serialising read -> gain -> write per bin.  Lanes other
-// than 0 compute a throw-away 17th bin from in-bounds LDS (the row after Y/N)
-// rather than branching: a masked branch costs the wave the same issue slots.
+// One frame's gain stage + real-IFFT packing for one lane.
+//
+// Bin ownership: lane i holds the 8 mirror pairs (k, M - k), k = i + L j
+// (j < 8), i.e. bins [0, M/2) and (M/2, M] once each, plus bin M/2 (its own
+// mirror) as a 17th item that every lane of the cell evaluates alike (only
+// lane 0's is used).  The inverse real FFT is a complex IFFT of length M of
+//   Z'[k] = (X_k + X*_{M-k}) + i (X_k - X*_{M-k}) e^{2πi k/NFFT},
+// and both halves of a pair come out of one lane:
+//   S = X_k + X*_{M-k}, D = X_k - X*_{M-k}, P = D e^{2πi k/NFFT}
+//   Z'[k] = S + i P,   Z'[M - k] = conj(S) + i conj(P)
+// Z'[k] (class i, index j) stays in the lane; Z'[M - k] = Z'[(L - i) + L (15 - j)]
+// goes to lane (L - i) mod L through a 9-entry LDS slot per lane.  Lane 0
+// keeps the DC/Nyquist pair (Im ignored, as irfft does) and bin M/2, whose
+// Z' = 2 conj(X_{M/2}).
+// The Y / gamma row pointers are __restrict__, so the scheduler may issue the
+// bins' reads up front and interleave the independent gain chains.
 template <int NFFT, int ALGO, bool OUT>
-__device__ __forceinline__ void gain_row(const float2* __restrict__ yr, const float* __restrict__ nr,
-                                         cf* __restrict__ sb, float (&rr)[17], float alpha_t,
-                                         const CellParam& cpar, float* __restrict__ grow, int i) {
+__device__ __forceinline__ void gain_pack(const float2* __restrict__ ylo, const float* __restrict__ glo,
+                                          const float2* __restrict__ yhi, const float* __restrict__ ghi,
+                                          const float2* __restrict__ ymid, const float* __restrict__ gmid,
+                                          cf (&z)[16], cf* __restrict__ xw, float (&rr)[17],
+                                          float alpha_t, const CellParam& cpar, cf base,
+                                          float* __restrict__ grow, int i) {
     constexpr int L = Geo<NFFT>::L, M = Geo<NFFT>::M;
-    float2 y[17];
-    float n[17];
+    // yhi / ghi point at bin M - i - 7L: bin M - i - L j is index L (7 - j).
+    // The next pair's four reads are issued before this pair's gains and a
+    // compiler memory fence keeps later reads from being hoisted further: the
+    // inputs of at most two pairs are live (register budget of 4 waves/SIMD).
+    float2 ya = ylo[0], yb = yhi[L * 7];
+    float ga = glo[0], gb = ghi[L * 7];
 #pragma unroll
-    for (int j = 0; j < 17; ++j) {
-        const int kk = (j < 16) ? L * j : M;  // k - i
-        y[j] = yr[kk];
-        n[j] = nr[kk];
-    }
-#pragma unroll
-    for (int j = 0; j < 17; ++j) {
-        const int kk = (j < 16) ? L * j : M;
-        float g;
-        const cf Sj = gain_bin<ALGO>(y[j], n[j], rr[j], alpha_t, cpar, g);
-        if (j < 16 || i == 0) {
-            sb[kk] = Sj;
-            if (OUT && grow) grow[kk] = g;
+    for (int j = 0; j < 8; ++j) {
+        float2 yan, ybn;
+        float gan, gbn;
+        if (j < 7) {
+            yan = ylo[L * (j + 1)];
+            gan = glo[L * (j + 1)];
+            ybn = yhi[L * (6 - j)];
+            gbn = ghi[L * (6 - j)];
+        } else {
+            yan = ymid[0];
+            gan = gmid[0];
+        }
+        asm volatile("" ::: "memory");
+        float g0, g1;
+        cf A = gain_bin<ALGO>(ya, ga, rr[j], alpha_t, cpar, g0);
+        cf Bm = gain_bin<ALGO>(yb, gb, rr[8 + j], alpha_t, cpar, g1);
+        if (OUT && grow) {
+            grow[i + L * j] = g0;
+            grow[M - i - L * j] = g1;
+        }
+        if (j == 0 && i == 0) {  // irfft ignores Im of DC and Nyquist
+            A.y = 0.0f;
+            Bm.y = 0.0f;
+        }
+        const float sx = A.x + Bm.x, sy = A.y - Bm.y;
+        const float dx = A.x - Bm.x, dy = A.y + Bm.y;
+        // packing rotor e^{2πi (i + L j)/NFFT} = base * W32^j
+        const cf w = (j == 0) ? base : cmul(base, cmk(Rot32::c[j], Rot32::s[j]));
+        const float px = fmaf(dx, w.x, -dy * w.y), py = fmaf(dx, w.y, dy * w.x);
+        z[j] = cmk(sx - py, sy + px);
+        xw[j] = cmk(sx + py, px - sy);  // Z'[M - k] for the mirror lane
+        ya = yan;
+        ga = gan;
+        if (j < 7) {
+            yb = ybn;
+            gb = gbn;
         }
     }
-}
-
-// gain_row with the frame's bins already in registers (CSE_DIRECT_ROWS)
-template <int NFFT, int ALGO, bool OUT>
-__device__ __forceinline__ void gain_row_regs(const float2 (&y)[17], const float (&n)[17],
-                                              cf* __restrict__ sb, float (&rr)[17], float alpha_t,
-                                              const CellParam& cpar, float* __restrict__ grow,
-                                              int i) {
-    constexpr int L = Geo<NFFT>::L, M = Geo<NFFT>::M;
-#pragma unroll
-    for (int j = 0; j < 17; ++j) {
-        const int kk = (j < 16) ? L * j : M;
-        float g;
-        const cf Sj = gain_bin<ALGO>(y[j], n[j], rr[j], alpha_t, cpar, g);
-        if (j < 16 || i == 0) {
-            sb[kk] = Sj;
-            if (OUT && grow) grow[kk] = g;
-        }
-    }
+    float gm;
+    const cf Sm = gain_bin<ALGO>(ya, ga, rr[16], alpha_t, cpar, gm);
+    if (OUT && grow && i == 0) grow[M / 2] = gm;
+    xw[8] = cmk(2.0f * Sm.x, -2.0f * Sm.y);
 }
 
 template <int NFFT, int HOP, int ALGO, bool OUT>
@@ -436,17 +367,18 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                                        unsigned char* smem) {
     using G = Geo<NFFT>;
     using W = WG<NFFT>;
-    constexpr int M = G::M, L = G::L, B = G::B, SP = G::SP, TR = W::TR;
+    constexpr int M = G::M, L = G::L, B = G::B, SP = G::SP, MH = M / 2;
     constexpr int R = NFFT / HOP;       // frames overlapping one sample
     constexpr int F = 2 * HOP / SP;     // samples a lane retires per frame
     constexpr int PEND = 32 - F;        // overlap-add sums carried to the next frame
     static_assert(F >= 2 && F <= 32 && (F % 2) == 0, "hop/n_fft combination");
+    // gamma floor of each algorithm (wiener_filter.py:122, mmse.py:71, advanced_mmse.py:207)
+    constexpr float EPS = (ALGO == CSE_ALGO_MMSE) ? 1e-12f : 1e-10f;
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int cs = lane / L, i = lane % L;
     const int cslot = wave * G::CPW + cs;
-    const int creg = W::OFF_CELLS + cslot * W::CREG;   // byte offset of my cell's region
-    const cf* tw1 = (const cf*)(smem + W::OFF_TW);
+    const int creg = cslot * W::CREG;   // byte offset of my cell's region
 
     // ---- the shared rows of this workgroup (first cell's; host-validated)
     const int len = (int)a.len;
@@ -476,14 +408,14 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     // ---- workgroup tables: pass-1 twiddles e^{2πi i b/M} [b-1][i], lane
     // constants [i], cell parameters [slot]
     for (int e = tid; e < 15 * W::TWL; e += W::THREADS) {
-        const int b = 1 + e / W::TWL, ii = e % W::TWL;
+        const int b = 1 + e % 15, ii = e / 15;
         double s, c;
         sincospi(2.0 * (double)(ii * b) / (double)M, &s, &c);
-        ((cf*)(smem + W::OFF_TW))[e] = cmk((float)c, (float)s);
+        ((cf*)(smem + W::OFF_TW))[ii * 18 + b - 1] = cmk((float)c, (float)s);
     }
-    // lane tables: packing rotor e^{2πi ii/NFFT}; window w(n)/NFFT at the
-    // lane's sample slots q (n = SP*(q>>1) + off + (q&1)); for 512/256 the
-    // reciprocal closed-form wss 0.75 + 0.25 cos(2π n/256) at its retired slots
+    // lane tables: packing rotor e^{2πi ii/NFFT}; window w(n)/NFFT at the lane's sample slots q
+    // (n = SP*(q>>1) + off + (q&1)); for 512/256 the reciprocal closed-form wss
+    // 0.75 + 0.25 cos(2π n/256) at its retired slots
     for (int e = tid; e < L * 32; e += W::THREADS) {
         const int ii = e / 32, q = e % 32;
         const int bb = (L == 16) ? ii : (ii & 15), hh = (L == 16) ? 0 : (ii >> 4);
@@ -494,9 +426,9 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             ((float*)(smem + W::OFF_IWS))[ii * W::ISTR + q] =
                 (float)(1.0 / (0.75 + 0.25 * cospi(2.0 * (double)n / 256.0)));
         if (q == 0) {
-            double sn, cs;
-            sincospi(2.0 * (double)ii / (double)NFFT, &sn, &cs);
-            ((cf*)(smem + W::OFF_LC))[ii] = cmk((float)cs, (float)sn);
+            double sn, cn;
+            sincospi(2.0 * (double)ii / (double)NFFT, &sn, &cn);
+            ((cf*)(smem + W::OFF_LC))[ii] = cmk((float)cn, (float)sn);
         }
     }
     for (int c = tid; c < W::CPWG; c += W::THREADS) {
@@ -513,52 +445,9 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         ((CellParam*)(smem + W::OFF_CP))[c] = prm;
     }
 
-#if CSE_DIRECT_ROWS
-    // ---- per-lane Y/N bins of frame t in registers (loaded one frame ahead);
-    // lanes other than 0 load the Nyquist bin too (same address, discarded)
-    float2 yv[17];
-    float nv[17];
-    auto load_yn = [&](int t) {
-        const float2* yt = Ybase + (int64_t)t * B;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) yv[j] = yt[i + L * j];
-        yv[16] = yt[M];
-        if (nstride || t == 0) {  // a static noise row is loaded once
-            const float* nt = Nbase + (int64_t)t * nstride;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) nv[j] = nt[i + L * j];
-            nv[16] = nt[M];
-        }
-    };
-    // ---- per-wave clean rows (double-buffered, wave-private: no barrier)
-    constexpr int CPL = W::HMAX / 64;
-    double pcd[CPL];
-    float* cwave = (float*)(smem + W::OFF_C + wave * W::CBUF);
-    auto load_c = [&](int t) {
-#pragma unroll
-        for (int u = 0; u < CPL; ++u) {
-            const int j = lane + 64 * u;
-            const int o = t * HOP - NFFT / 2 + j + lag;  // clean sample scored against y[o - lag]
-            pcd[u] = (j < HOP && cbase && o >= 0 && o < len) ? cbase[o] : 0.0;
-        }
-    };
-    auto store_c = [&](int t) {
-        float* crow = cwave + (t & 1) * W::HMAX;
-#pragma unroll
-        for (int u = 0; u < CPL; ++u) {
-            const int j = lane + 64 * u;
-            if (j < HOP) crow[j] = (float)pcd[u];
-        }
-    };
-    load_yn(0);
-    load_c(0);
-    store_c(0);
-    load_c(1);
-    __syncthreads();  // workgroup tables written
-#else
     // ---- row staging: thread tid owns Y/N elements tid + u*THREADS, clean tid + u*THREADS
     float2 py[W::YPT];
-    float pn[W::YPT];
+    float pn[W::YPT];  // N (SS) or 1/max(N, eps); a static row stays here for the whole cell
     // clean samples stay f64 in flight: converting at load time made the
     // compiler wait (vmcnt(0)) for every row load right after issuing them
     double pc[W::CPT];
@@ -580,17 +469,21 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             pc[u] = (j < HOP && cbase && o >= 0 && o < len) ? cbase[o] : 0.0;
         }
     };
-    // rows of frame t live in buffer t&1 (static noise: written to both once)
+    // rows of frame t live in buffer t&1: Y and gamma = max(|Y|^2 inv, eps)
+    // (the noise row itself for SS)
     auto store_rows = [&](int t) {  // registers -> LDS rows of frame t
         if (t < nf) {
             float2* yrow = (float2*)(smem + W::OFF_Y + (t & 1) * W::YROW);
-            float* nrow = (float*)(smem + W::OFF_N + (t & 1) * W::NROW);
+            float* grow = (float*)(smem + W::OFF_G + (t & 1) * W::GROW);
 #pragma unroll
             for (int u = 0; u < W::YPT; ++u) {
                 const int k = tid + u * W::THREADS;
                 if (k < B) {
                     yrow[k] = py[u];
-                    if (nstride) nrow[k] = pn[u];
+                    if (ALGO == CSE_ALGO_SS)
+                        grow[k] = pn[u];
+                    else
+                        grow[k] = fmaxf((py[u].x * py[u].x + py[u].y * py[u].y) * pn[u], EPS);
                 }
             }
         }
@@ -602,16 +495,15 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         }
     };
     if (!nstride) {
-        for (int k = tid; k < B; k += W::THREADS) {
-            const float v = Nbase[k];
-            ((float*)(smem + W::OFF_N))[k] = v;
-            ((float*)(smem + W::OFF_N + W::NROW))[k] = v;
+#pragma unroll
+        for (int u = 0; u < W::YPT; ++u) {
+            const int k = tid + u * W::THREADS;
+            if (k < B) pn[u] = Nbase[k];
         }
     }
     load_rows(0);
     store_rows(0);
     load_rows(1);
-#endif
 
     const int b2 = (L == 16) ? i : (i & 15);
     const int h2 = (L == 16) ? 0 : (i >> 4);
@@ -629,147 +521,123 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     for (int t = 0; t < nf + R - 1; ++t) {
         float x[32];  // this frame's windowed IFFT samples (0 in flush frames)
         if (t < nf) {
-#if !CSE_DIRECT_ROWS
             // the one workgroup barrier per frame: rows(t) (stored during frame
             // t-1) are visible, and nobody still reads buffer (t+1)&1
-            if (!(CSE_ABLATE & 8)) __syncthreads();
-#endif
+            __syncthreads();
             CSE_MARK("gain");
-            if (CSE_PRIO & 1) __builtin_amdgcn_s_setprio(CSE_PRIO_LEVEL);
-            // ---------------- gain stage: S = Y * G into my cell's LDS row
-            {
-                const CellParam cpar =
-                    *(const CellParam*)(smem + opaque(W::OFF_CP + 32 * cslot));
-                const float alpha_t = (t == 0) ? 0.0f : cpar.p0;  // see gain_wiener
-                cf* sb = (cf*)(smem + opaque(creg + 8 * i));   // &S[i]
-#if CSE_DIRECT_ROWS
-                gain_row_regs<NFFT, ALGO, OUT>(yv, nv, sb, rr, alpha_t, cpar,
-                                               (OUT && gout) ? gout + t * B + i : nullptr, i);
-            }
-            if (CSE_PREFETCH_AT == 0 && t + 1 < nf) load_yn(t + 1);  // in flight during the IFFT
-#else
-                const float2* yr =
-                    (const float2*)(smem + opaque(W::OFF_Y + (t & 1) * W::YROW + 8 * i));
-                const float* nr =
-                    (const float*)(smem + opaque(W::OFF_N + (t & 1) * W::NROW + 4 * i));
-                gain_row<NFFT, ALGO, OUT>(yr, nr, sb, rr, alpha_t, cpar,
-                                          (OUT && gout) ? gout + t * B + i : nullptr, i);
-            }
-#endif
-            CSE_MARK("rows");
-            if (CSE_PRIO & 1) __builtin_amdgcn_s_setprio(0);
-#if !CSE_DIRECT_ROWS
-            if (!(CSE_ABLATE & 64)) {
-                store_rows(t + 1);  // other buffer: its last readers passed this frame's barrier
-                load_rows(t + 2);
-            }
-#endif
-            wave_sync();  // my wave's S rows complete (cells never span waves)
-
-            CSE_MARK("pass1");
-            if (CSE_PRIO & 2) __builtin_amdgcn_s_setprio(1);
-            // ---------------- pass 1: real-IFFT packing + DFT16 over j -----
-            // Z'[k] = (X_k + X*_{M-k}) + i (X_k - X*_{M-k}) e^{2πi k/NFFT}
+            // the VALU-dense gain stage issues ahead of other waves' LDS-bound
+            // IFFT stages, whose latency then overlaps it (r01: 33.3 -> 31.5 ms)
+            __builtin_amdgcn_s_setprio(1);
             cf z[16];
             {
+                const CellParam cpar = *(const CellParam*)(smem + opaque(W::OFF_CP + 32 * cslot));
+                const float alpha_t = (t == 0) ? 0.0f : cpar.p0;  // see gain_wiener
                 const cf base = *(const cf*)(smem + opaque(W::OFF_LC + 8 * i));
-                const cf* sa = (const cf*)(smem + opaque(creg + 8 * i));                   // S[i + L j]
-                const cf* sm = (const cf*)(smem + opaque(creg + 8 * (M - i - 15 * L)));   // S[M - i - L j]
-                // rotor tw_j = e^{2πi (i + L j)/NFFT} = base * W32^j; W32^8 = i gives
-                // tw_{j+8} = i tw_j, so only j < 8 is computed and, with
-                // P = D tw:  z_j = S + i P_j (j < 8),  z_{j+8} = S - P'_{j} (P' = D tw_j)
-                cf tw[8];
-                tw[0] = base;
-#pragma unroll
-                for (int j = 1; j < 8; ++j) tw[j] = cmul(base, cmk(Rot32::c[j], Rot32::s[j]));
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    cf A = sa[L * j];
-                    cf Bm = sm[L * (15 - j)];
-                    if (j == 0 && i == 0) {  // irfft ignores Im of DC and Nyquist
-                        A.y = 0.0f;
-                        Bm.y = 0.0f;
-                    }
-                    // S = A + conj(Bm), D = A - conj(Bm)
-                    const float sx = A.x + Bm.x, sy = A.y - Bm.y;
-                    const float dx = A.x - Bm.x, dy = A.y + Bm.y;
-                    const cf w = tw[j & 7];
-                    if (j < 8) {  // S + i (D w)
-                        z[j] = cmk(fmaf(-dx, w.y, fmaf(-dy, w.x, sx)), fmaf(dx, w.x, fmaf(-dy, w.y, sy)));
-                    } else {      // S + i (D i w) = S - D w
-                        z[j] = cmk(fmaf(-dx, w.x, fmaf(dy, w.y, sx)), fmaf(-dx, w.y, fmaf(-dy, w.x, sy)));
-                    }
-                }
+                const int yb = W::OFF_Y + (t & 1) * W::YROW, gb = W::OFF_G + (t & 1) * W::GROW;
+                // mirror halves: lane i's slot e (9 entries, 72 B) receives
+                // Z'[M - i - L e] (e < 8) and Z'[M/2] (e = 8); lane q takes
+                // z[s] (s >= 8) = Z'[q + L s] from lane (L - q) mod L, entry 15 - s
+                // (lane 0: its own entry 16 - s, entry 8 = Z'[M/2] for s = 8)
+                gain_pack<NFFT, ALGO, OUT>(
+                    (const float2*)(smem + opaque(yb + 8 * i)), (const float*)(smem + opaque(gb + 4 * i)),
+                    (const float2*)(smem + opaque(yb + 8 * (M - i - 7 * L))),
+                    (const float*)(smem + opaque(gb + 4 * (M - i - 7 * L))),
+                    (const float2*)(smem + yb + 8 * MH), (const float*)(smem + gb + 4 * MH), z,
+                    (cf*)(smem + opaque(creg + 72 * i)), rr, alpha_t, cpar, base,
+                    (OUT && gout) ? gout + t * B : nullptr, i);
             }
-            if (!(CSE_ABLATE & 2)) idft16(z);
+            __builtin_amdgcn_s_setprio(0);
+            CSE_MARK("xchg");
+            wave_sync();  // my wave's mirror entries written
             {
-                if constexpr (W::HALF_TABLES) {
-                    const cf* tw = (const cf*)((const unsigned char*)tw1 + opaque(8 * b2));
+                const int partner = (L - i) & (L - 1);
+                const cf* xr = (const cf*)(smem + opaque(creg + 72 * partner + (i == 0 ? 8 : 0)));
 #pragma unroll
-                    for (int b = 1; b < 16; ++b) {
-                        const cf t = tw[(b - 1) * W::TWL];
-                        const cf th = cmul(t, cmk(Rot32::c[b], Rot32::s[b]));  // x W32^b
-                        z[b] = cmul(z[b], h2 ? th : t);
-                    }
-                } else {
-                    const cf* tw = (const cf*)((const unsigned char*)tw1 + opaque(8 * i));
-#pragma unroll
-                    for (int b = 1; b < 16; ++b) z[b] = cmul(z[b], tw[(b - 1) * L]);
-                }
+                for (int s = 8; s < 16; ++s) z[s] = xr[15 - s];
             }
-            wave_sync();  // my wave's S reads are issued before the transpose overwrites
-            {
-                cf* tw_ = (cf*)(smem + opaque(creg + 8 * i));   // V[b][i] at b*TR + i
-#pragma unroll
-                for (int b = 0; b < 16; ++b)
-                    if (!(CSE_ABLATE & 128)) tw_[b * TR] = z[b];
-            }
-            wave_sync();  // transpose block written
-#if CSE_DIRECT_ROWS
-            if (CSE_PREFETCH_AT == 1 && t + 1 < nf) load_yn(t + 1);
-#endif
+            CSE_MARK("rows");
+            store_rows(t + 1);  // other buffer: its last readers passed this frame's barrier
+            load_rows(t + 2);
 
+            CSE_MARK("pass1");
+            {
+                // pass-1 twiddles e^{2πi i' b/M}, b = 1..15, of my column (per-lane
+                // row of 18 complex: 8 ds_read_b128), issued ahead of the DFT
+                const float4* twr = (const float4*)(smem + opaque(W::OFF_TW + 144 * ((L == 16) ? i : b2)));
+                float4 t4[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) t4[k] = twr[k];
+                idft16(z);
+#pragma unroll
+                for (int b = 1; b < 16; ++b) {
+                    const float4 q4 = t4[(b - 1) >> 1];
+                    const cf t = ((b - 1) & 1) ? cmk(q4.z, q4.w) : cmk(q4.x, q4.y);
+                    if constexpr (W::HALF_TABLES) {  // column i = b2 + 16 h2: x W32^{h2 b}
+                        const cf th = cmul(t, cmk(Rot32::c[b], Rot32::s[b]));
+                        z[b] = cmul(z[b], h2 ? th : t);
+                    } else {
+                        z[b] = cmul(z[b], t);
+                    }
+                }
+            }
             CSE_MARK("pass2");
-            if (CSE_PRIO & 4) __builtin_amdgcn_s_setprio(1);
-            // ---------------- pass 2: DFT over the lane index --------------
+            // ---------------- pass 2: transpose in two column rounds, DFT over lanes
+            // Lane (b2, h2) needs row b2 of V[b][i]: the DFT16 (512) / DFT32
+            // (1024) input over the pass-1 lane index.  Round A moves the columns
+            // i' = i mod 16 < 8 (written by those lanes), round B i' >= 8; every
+            // lane reads 8 (16) entries per round.  Block: 16 rows x TS complex,
+            // row stride TS = 9 (512) / 18 (1024): the transposed reads of a
+            // 16-lane group hit distinct bank pairs.
             cf v[16];
             {
-                const cf* tr = (const cf*)(smem + opaque(creg + 8 * TR * b2));   // row V[b2][.]
-                if (CSE_ABLATE & 128) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) v[r] = z[r];
-                } else if (L == 16) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) v[r] = tr[r];
-                } else {  // DFT32 = butterfly (lo +- hi) * W32^{r h}, then DFT16
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const cf lo = tr[r];
-                        const cf hi = tr[r + 16];
+                constexpr int TS = (L == 16) ? 9 : 18, COLS = (L == 16) ? 1 : 2;
+                wave_sync();  // my wave's mirror reads are issued before the transpose overwrites
+                const int ip = i & 15;
+                // entry (b, COLS (i' mod 8) + h): at 1024 lo = V[b][i'] and
+                // hi = V[b][i' + 16] sit side by side
+                cf* tw_ = (cf*)(smem + opaque(creg + 8 * (COLS * (ip & 7) + h2)));  // + 8 TS b
+                const cf* tr = (const cf*)(smem + opaque(creg + 8 * TS * b2));       // + 8 COLS r
+                // DFT32 (1024) = radix-2 decimation in frequency on the read side:
+                // lane (b2, h2) takes U_h2[i'] = (lo + (-1)^h2 hi) W32^{i' h2},
+                // then a DFT16 over i'
+                auto take = [&](int r, const cf* p) {
+                    if constexpr (L == 32) {
+                        const cf lo = p[0], hi = p[1];
                         const cf u = h2 ? csub(lo, hi) : cadd(lo, hi);
-                        v[r] = h2 ? cmul(u, cmk(Rot32::c[r], Rot32::s[r])) : u;
+                        return h2 ? cmul(u, cmk(Rot32::c[r], Rot32::s[r])) : u;
+                    } else {
+                        return p[0];
                     }
+                };
+                if (ip < 8) {
+#pragma unroll
+                    for (int b = 0; b < 16; ++b) tw_[b * TS] = z[b];
                 }
+                wave_sync();
+#pragma unroll
+                for (int r = 0; r < 8; ++r) v[r] = take(r, tr + COLS * r);
+                wave_sync();
+                if (ip >= 8) {
+#pragma unroll
+                    for (int b = 0; b < 16; ++b) tw_[b * TS] = z[b];
+                }
+                wave_sync();
+#pragma unroll
+                for (int r = 0; r < 8; ++r) v[8 + r] = take(8 + r, tr + COLS * r);
             }
-            if (!(CSE_ABLATE & 2)) idft16(v);
+            idft16(v);
             CSE_MARK("window");
             // the synthesis window (/n_fft) is applied by the overlap-add FMAs below
 #pragma unroll
             for (int q = 0; q < 32; ++q) x[q] = (q & 1) ? v[q >> 1].y : v[q >> 1].x;
         } else {
-#if !CSE_DIRECT_ROWS
             __syncthreads();  // flush frames: clean row t visible, row t-1 reads done
             store_rows(t + 1);
             load_rows(t + 2);
-#endif
 #pragma unroll
             for (int q = 0; q < 32; ++q) x[q] = 0.0f;
         }
 
-#if CSE_DIRECT_ROWS
-        if (CSE_PREFETCH_AT == 2 && t + 1 < nf) load_yn(t + 1);
-#endif
-        if (CSE_PRIO & 6) __builtin_amdgcn_s_setprio(0);
         CSE_MARK("retire");
         // ---------------- overlap-add + retire HOP finished samples ---------
         // slot q < F of this frame completes output position t*HOP + n(q):
@@ -779,25 +647,31 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         // sum the covering windows explicitly.
         // windowed overlap-add: x * w(n)/n_fft folded into the accumulating FMAs
         // (x = 0 in flush frames, so they leave the sums unchanged)
-        float done[F];
+        // the lane's window slots: ds_read_b128 from its 16-B aligned table row
+        float wv[W::WSLOTS];
         {
-            const float* wt = (const float*)__builtin_assume_aligned(
-                smem + opaque(W::OFF_WIN + 4 * W::WSTR * i), 16);
+            const float4* w4 = (const float4*)(smem + opaque(W::OFF_WIN + 4 * W::WSTR * i));
 #pragma unroll
-            for (int q = 0; q < F; ++q) done[q] = fmaf(x[q], win_at<W>(wt, q), acc[q]);
-#pragma unroll
-            for (int q = 0; q < PEND; ++q)
-                acc[q] = fmaf(x[q + F], win_at<W>(wt, q + F), q + F < PEND ? acc[q + F] : 0.0f);
+            for (int k = 0; k < W::WSLOTS / 4; ++k) {
+                const float4 q4 = w4[k];
+                wv[4 * k] = q4.x;
+                wv[4 * k + 1] = q4.y;
+                wv[4 * k + 2] = q4.z;
+                wv[4 * k + 3] = q4.w;
+            }
         }
-        if (valid && !(CSE_ABLATE & 4)) {
+        auto win = [&](int q) {  // w(n)/NFFT at slot q (compile-time after unrolling)
+            return (W::HALF_TABLES && q >= 16) ? (1.0f / (float)M / 2.0f) - wv[q - 16] : wv[q];
+        };
+        float done[F];
+#pragma unroll
+        for (int q = 0; q < F; ++q) done[q] = fmaf(x[q], win(q), acc[q]);
+#pragma unroll
+        for (int q = 0; q < PEND; ++q) acc[q] = fmaf(x[q + F], win(q + F), q + F < PEND ? acc[q + F] : 0.0f);
+        if (valid) {
             const int o0 = t * HOP + off - NFFT / 2;  // output index of q = 0
-#if CSE_DIRECT_ROWS
-            const float* crow_t = (const float*)__builtin_assume_aligned(
-                smem + opaque(W::OFF_C + wave * W::CBUF + (t & 1) * W::HMAX * 4 + 4 * off), 8);
-#else
             const float* crow_t = (const float*)__builtin_assume_aligned(
                 smem + opaque(W::OFF_C + (t & 1) * W::HMAX * 4 + 4 * off), 8);
-#endif
             // frame t retires output positions [t*HOP - NFFT/2, (t+1)*HOP - NFFT/2)
             // interior: every slot o and its scored clean index o + lag lie in [0, len)
             const bool edge = (t < R - 1) || (t >= nf);
@@ -807,10 +681,15 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             const bool head = want_y && lo < out_len;                      // uniform
             float inv[F];
             if (R == 2) {
-                const float* it = (const float*)__builtin_assume_aligned(
-                    smem + opaque(W::OFF_IWS + 4 * W::ISTR * i), 16);
+                const float4* it = (const float4*)(smem + opaque(W::OFF_IWS + 4 * W::ISTR * i));
 #pragma unroll
-                for (int q = 0; q < F; ++q) inv[q] = it[q];
+                for (int k = 0; k < F / 4; ++k) {
+                    const float4 q4 = it[k];
+                    inv[4 * k] = q4.x;
+                    inv[4 * k + 1] = q4.y;
+                    inv[4 * k + 2] = q4.z;
+                    inv[4 * k + 3] = q4.w;
+                }
             } else {
 #pragma unroll
                 for (int q = 0; q < F; ++q) inv[q] = (R == 4) ? (1.0f / 1.5f) : (1.0f / 3.0f);
@@ -825,11 +704,11 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     const float y = done[q] * inv[q];
                     chk = fmaf(y, 0.0f, chk);
                     if (head && yout && o0 + n < out_len) yout[o0 + n] = y;
-                    const float d = crow_t[n] - fminf(fmaxf(y, -1.0f), 1.0f);
+                    const float2 c2 = *(const float2*)(crow_t + SP * (q >> 1));
+                    const float d = ((q & 1) ? c2.y : c2.x) - fminf(fmaxf(y, -1.0f), 1.0f);
                     part = fmaf(d, d, part);
                 }
             } else {
-                const float* wt = (const float*)(smem + opaque(W::OFF_WIN + 4 * W::WSTR * i));
 #pragma unroll
                 for (int q = 0; q < F; ++q) {
                     const int n = SP * (q >> 1) + (q & 1);  // + off: position inside frame t
@@ -841,7 +720,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                         for (int r = 0; r < R; ++r) {
                             const int tr = t - r;
                             if (tr >= 0 && tr < nf) {
-                                const float w = win_at<W>(wt, q + 2 * r * (HOP / SP)) * NFFT;
+                                const float w = win(q + 2 * r * (HOP / SP)) * NFFT;
                                 wss = fmaf(w, w, wss);
                             }
                         }
@@ -859,14 +738,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 }
             }
             sse += (double)part;
-        } else if (CSE_ABLATE & 4) {
-#pragma unroll
-            for (int q = 0; q < F; ++q) asm volatile("" ::"v"(done[q]));
         }
-#if CSE_DIRECT_ROWS
-        store_c(t + 1);  // buffer (t+1)&1: this wave's last read of it was frame t-1
-        load_c(t + 2);
-#endif
         CSE_MARK("end");
     }
 

@@ -4,7 +4,7 @@ Compiles cse_enhance.hip with -DCSE_MARKS (asm comment markers between the
 stages), extracts the kernel's ISA and counts instructions between markers,
 per (hop, algorithm) specialisation, by class.  Analysis only.
 
-    python tools/isa_sections.py [kernel-substring]
+    python tools/isa_sections.py [kernel-substring [source]]
 """
 import collections
 import os
@@ -37,10 +37,11 @@ def classify(op):
     return "other"
 
 
-def main(kname="enhance_kernelILi512ELb0E", extra=()):
+def main(kname="enhance_kernelILi512ELb0E", src=SRC, extra=()):
     out = "/tmp/cse_marks.s"
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I" + os.path.join(REPO, "include"),
-                    "-DCSE_MARKS", "-fno-slp-vectorize", "-S", "--cuda-device-only", SRC, "-o", out, *extra], check=True)
+                    "-I" + os.path.join(REPO, "classical_speech_enhancement_amd", "csrc"),
+                    "-DCSE_MARKS", "-fno-slp-vectorize", "-S", "--cuda-device-only", src, "-o", out, *extra], check=True)
     lines = open(out).read().splitlines()
     start = next(i for i, l in enumerate(lines) if l.startswith("_ZN3cse14" + kname.split("14", 1)[-1])
                  or (kname in l and l.endswith(":") is False and l.startswith("_Z") and ":" in l))
@@ -71,4 +72,4 @@ def main(kname="enhance_kernelILi512ELb0E", extra=()):
 
 
 if __name__ == "__main__":
-    main(*(sys.argv[1:2] or []))
+    main(*(sys.argv[1:3] or []))

@@ -7,7 +7,7 @@ C="$1"; shift
 for lib in "$@"; do
   d=gpurun_out/pmc_libs/${lib%.so}
   mkdir -p $d
-  CSE_BENCH_NOCHECK=1 CSE_LIB=classical_speech_enhancement_amd/$lib timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $d -o run -- python3 bench.py --steps 1 --warmup 0 --pairs 8 --no-cpu-baseline > $d.log 2>&1 || { echo "$lib failed"; tail -3 $d.log; exit 1; }
+  CSE_BENCH_NOCHECK=1 CSE_LIB=classical_speech_enhancement_amd/$lib timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $d -o run -- python3 bench.py --steps 1 --warmup 0 --pairs ${PAIRS:-8} --nfft ${NFFT:-512} --no-cpu-baseline --no-parity > $d.log 2>&1 || { echo "$lib failed"; tail -3 $d.log; exit 1; }
   python - "$d" "$lib" <<'PY'
 import csv, glob, sys
 acc = {}

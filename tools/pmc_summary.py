@@ -1,0 +1,117 @@
+"""Summarise a tools/profile_all.sh run into profiles/ (committed evidence).
+
+For every kernel of interest: rocprofv3 --kernel-trace --stats average duration
+and calls, and the PMC counters of the separate --pmc passes, per launch
+(counter sum over the profiled launches / launches).  HBM traffic per launch =
+(2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 (gfx950 correction, MI355X_MICROARCH.md
+HBM/rocprofv3 section: FETCH_SIZE counts half the bytes of wide streaming reads).
+VALU issue fraction = (2 x (VALU - TRANS) + 8 x TRANS) SIMD cycles over
+1024 SIMDs x GRBM_GUI_ACTIVE / 8 (rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs).
+
+    python tools/pmc_summary.py TAG ROUND [UNITS_512 UNITS_1024]
+
+Writes profiles/{ROUND}_kernels.json (all kernels) and, when the launch sizes
+are given, profiles/pmc_enhance512_{ROUND}.json / pmc_enhance1024_{ROUND}.json,
+which bench.py reads (matched by units_per_launch) for roofline.traffic/valu.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+KERNELS = {"enhance512": "enhance_kernel<512, false>", "enhance1024": "enhance_kernel<1024, false>",
+           "stoi": "stoi_cells_kernel", "xcorr_lag": "xcorr_lag_kernel"}
+SIMDS, VALU_CYC, TRANS_CYC = 1024, 2, 8
+
+
+def stats(path):
+    out = {}
+    for r in csv.DictReader(open(path)):
+        out[r["Name"]] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
+                          "pct": float(r["Percentage"])}
+    return out
+
+
+def counters(pattern, kname):
+    """{counter: value per launch} over the matching dispatches of all pmc dirs."""
+    acc, disp = {}, {}
+    for f in glob.glob(pattern):
+        for r in csv.DictReader(open(f)):
+            if kname not in r["Kernel_Name"]:
+                continue
+            c = r["Counter_Name"]
+            acc[c] = acc.get(c, 0.0) + float(r["Counter_Value"])
+            disp.setdefault(c, set()).add(r["Dispatch_Id"])
+    return {c: v / len(disp[c]) for c, v in acc.items()}, {c: len(d) for c, d in disp.items()}
+
+
+def derive(pmc, kernel_ms):
+    d = {}
+    if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+        d["hbm_bytes_per_launch"] = (2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024
+    vi, tr, gui = pmc.get("SQ_INSTS_VALU"), pmc.get("SQ_INSTS_VALU_TRANS_F32", 0.0), pmc.get("GRBM_GUI_ACTIVE")
+    if vi and gui:
+        need = VALU_CYC * (vi - tr) + TRANS_CYC * tr
+        d["valu_issue_cycles"] = need
+        d["valu_frac"] = need / (SIMDS * gui / 8)
+        d["clock_ghz_profiled"] = gui / 8 / (kernel_ms / 1e3) / 1e9 if kernel_ms else None
+    if "SQ_WAVE_CYCLES" in pmc:
+        w = pmc["SQ_WAVE_CYCLES"]
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                  "SQ_ACTIVE_INST_LDS"):
+            if k in pmc:
+                d["share_" + k[3:].lower()] = pmc[k] / w
+    if "SQ_LDS_BANK_CONFLICT" in pmc and "SQ_INSTS_LDS" in pmc:
+        d["lds_conflict_cycles_per_lds_inst"] = pmc["SQ_LDS_BANK_CONFLICT"] / pmc["SQ_INSTS_LDS"]
+    return d
+
+
+def main(tag, rnd, units512=None, units1024=None):
+    base = os.path.join(REPO, "gpurun_out", f"prof_{tag}")
+    kt = {}
+    for name in ("512", "1024", "sweep"):
+        p = os.path.join(base, f"kt_{name}", "run_kernel_stats.csv")
+        if os.path.exists(p):
+            kt[name] = stats(p)
+    summary = {"round": rnd, "tag": tag, "commands": {
+        "kt512": "rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity",
+        "kt1024": "... bench.py --nfft 1024 --steps 3 --warmup 1 --no-cpu-baseline --no-parity",
+        "ktsweep": "... tools/bench_sweep.py --pairs 4 --reps 1",
+        "pmc": "one rocprofv3 --pmc pass per counter group (tools/profile_all.sh), bench.py --steps 1 --warmup 0"},
+        "kernel_stats": kt, "kernels": {}}
+    src = {"enhance512": ("512", "512"), "enhance1024": ("1024", "1024"), "stoi": ("sweep", "stoi"),
+           "xcorr_lag": ("sweep", "stoi")}
+    for key, kname in KERNELS.items():
+        ktname, pmcname = src[key]
+        ms = None
+        for n, v in kt.get(ktname, {}).items():
+            if kname in n:
+                ms = v["avg_ms"]
+        pmc, nd = counters(os.path.join(base, f"pmc_{pmcname}_*", "run_counter_collection.csv"), kname)
+        summary["kernels"][key] = {"kernel": kname, "kernel_ms_rocprof": ms, "pmc_per_launch": pmc,
+                                   "pmc_launches": nd, **derive(pmc, ms)}
+    os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
+    json.dump(summary, open(os.path.join(REPO, "profiles", f"{rnd}_kernels.json"), "w"), indent=1)
+    for key, units in (("enhance512", units512), ("enhance1024", units1024)):
+        if not units:
+            continue
+        k = summary["kernels"][key]
+        pmc = k["pmc_per_launch"]
+        out = {"kernel": "cse::" + k["kernel"], "round": rnd, "units_per_launch": int(units),
+               "kernel_ms": k["kernel_ms_rocprof"],
+               "hbm_bytes_per_launch": k.get("hbm_bytes_per_launch"),
+               "sq_insts_valu": pmc.get("SQ_INSTS_VALU"), "sq_insts_valu_trans": pmc.get("SQ_INSTS_VALU_TRANS_F32"),
+               "grbm_gui_active": pmc.get("GRBM_GUI_ACTIVE"),
+               "valu_frac": k.get("valu_frac"),
+               "source": f"profiles/{rnd}_kernels.json (tools/profile_all.sh {tag})"}
+        json.dump(out, open(os.path.join(REPO, "profiles", f"pmc_{key}_{rnd}.json"), "w"), indent=1)
+    for key, k in summary["kernels"].items():
+        print(key, "ms", k["kernel_ms_rocprof"], "valu_frac", k.get("valu_frac"),
+              "hbm MB", (k.get("hbm_bytes_per_launch") or 0) / 1e6,
+              "wait_inst", k.get("share_wait_inst_any"), "conf/lds", k.get("lds_conflict_cycles_per_lds_inst"))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
