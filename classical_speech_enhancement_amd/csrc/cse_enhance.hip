@@ -182,11 +182,13 @@ struct WG {
     static constexpr int HMAX = 256;                              // largest hop
     // per-cell LDS region: the mirror-exchange slots (9 complex per lane,
     // stride 72 B: the 16 lanes of a ds_write_b64 group hit disjoint banks)
-    // aliased with the half transpose block (16 x 9 / 18 complex).  Its size is an
-    // odd multiple of 128 B, so the two cells of a 32-lane ds_read_b64 group
-    // (n_fft 512) sit in disjoint bank halves of the transposed reads.
+    // aliased with the transpose block (16 rows x TS = L + 1 complex).  Its
+    // size is an odd multiple of 128 B, so the two cells of a 32-lane
+    // ds_read_b64 group (n_fft 512) sit in disjoint bank halves of the
+    // transposed reads.
+    static constexpr int TS = G::L + 1;
     static constexpr int XB = G::L * 9 * 8;
-    static constexpr int TB = 16 * ((G::L == 16) ? 9 : 18) * 8;
+    static constexpr int TB = 16 * TS * 8;
     static constexpr int CREG_RAW = XB > TB ? XB : TB;
     static constexpr int CREG_U = (CREG_RAW + 127) / 128;
     static constexpr int CREG = (CREG_U + (CREG_U % 2 ? 0 : 1)) * 128;
@@ -220,9 +222,10 @@ struct WG {
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
-// 4 workgroups (16 waves) per CU fit the LDS; the register budget then sets occupancy
-static_assert(4 * WG<512>::BYTES <= 163840, "n_fft=512 workgroups must fit 4 per CU");
-static_assert(4 * WG<1024>::BYTES <= 163840, "n_fft=1024 workgroups must fit 4 per CU");
+// the registers (3 waves/SIMD) set the occupancy: LDS must not cut it below
+// 3 workgroups (12 waves) per CU
+static_assert(3 * WG<512>::BYTES <= 163840, "n_fft=512 workgroups must fit 3 per CU");
+static_assert(3 * WG<1024>::BYTES <= 163840, "n_fft=1024 workgroups must fit 3 per CU");
 static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
               WG<1024>::CPWG == CSE_CELLS_PER_GROUP(1024), "cse.h slot-group size");
 
@@ -581,49 +584,35 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 }
             }
             CSE_MARK("pass2");
-            // ---------------- pass 2: transpose in two column rounds, DFT over lanes
+            // ---------------- pass 2: transpose, DFT over lanes
             // Lane (b2, h2) needs row b2 of V[b][i]: the DFT16 (512) / DFT32
-            // (1024) input over the pass-1 lane index.  Round A moves the columns
-            // i' = i mod 16 < 8 (written by those lanes), round B i' >= 8; every
-            // lane reads 8 (16) entries per round.  Block: 16 rows x TS complex,
-            // row stride TS = 9 (512) / 18 (1024): the transposed reads of a
-            // 16-lane group hit distinct bank pairs.
+            // (1024) input over the pass-1 lane index.  Block: 16 rows x TS
+            // complex, entry (b, i); row stride TS = L + 1: the transposed reads
+            // of a 16-lane group hit distinct bank pairs.
             cf v[16];
             {
-                constexpr int TS = (L == 16) ? 9 : 18, COLS = (L == 16) ? 1 : 2;
+                constexpr int TS = W::TS;
                 wave_sync();  // my wave's mirror reads are issued before the transpose overwrites
-                const int ip = i & 15;
-                // entry (b, COLS (i' mod 8) + h): at 1024 lo = V[b][i'] and
-                // hi = V[b][i' + 16] sit side by side
-                cf* tw_ = (cf*)(smem + opaque(creg + 8 * (COLS * (ip & 7) + h2)));  // + 8 TS b
-                const cf* tr = (const cf*)(smem + opaque(creg + 8 * TS * b2));       // + 8 COLS r
-                // DFT32 (1024) = radix-2 decimation in frequency on the read side:
-                // lane (b2, h2) takes U_h2[i'] = (lo + (-1)^h2 hi) W32^{i' h2},
-                // then a DFT16 over i'
-                auto take = [&](int r, const cf* p) {
-                    if constexpr (L == 32) {
-                        const cf lo = p[0], hi = p[1];
+                cf* tw_ = (cf*)(smem + opaque(creg + 8 * i));              // + 8 TS b
+                const cf* tr = (const cf*)(smem + opaque(creg + 8 * TS * b2));  // + 8 r
+#pragma unroll
+                for (int b = 0; b < 16; ++b) tw_[b * TS] = z[b];
+                wave_sync();
+                if constexpr (L == 32) {
+                    // DFT32 over i = i' + 16 h: radix-2 decimation in frequency on
+                    // the read side, lane (b2, h2) takes lo = V[b2][i'], hi =
+                    // V[b2][i' + 16]: U_h2[i'] = (lo + (-1)^h2 hi) W32^{i' h2},
+                    // then a DFT16 over i'
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const cf lo = tr[r], hi = tr[r + 16];
                         const cf u = h2 ? csub(lo, hi) : cadd(lo, hi);
-                        return h2 ? cmul(u, cmk(Rot32::c[r], Rot32::s[r])) : u;
-                    } else {
-                        return p[0];
+                        v[r] = h2 ? cmul(u, cmk(Rot32::c[r], Rot32::s[r])) : u;
                     }
-                };
-                if (ip < 8) {
+                } else {
 #pragma unroll
-                    for (int b = 0; b < 16; ++b) tw_[b * TS] = z[b];
+                    for (int r = 0; r < 16; ++r) v[r] = tr[r];
                 }
-                wave_sync();
-#pragma unroll
-                for (int r = 0; r < 8; ++r) v[r] = take(r, tr + COLS * r);
-                wave_sync();
-                if (ip >= 8) {
-#pragma unroll
-                    for (int b = 0; b < 16; ++b) tw_[b * TS] = z[b];
-                }
-                wave_sync();
-#pragma unroll
-                for (int r = 0; r < 8; ++r) v[8 + r] = take(8 + r, tr + COLS * r);
             }
             idft16(v);
             CSE_MARK("window");

@@ -61,13 +61,11 @@ def job_specs(n_pairs, algorithms=None, grids=None, n_fft=None):
     order with the last key fastest)."""
     grids = grids or ALGORITHM_GRIDS
     algorithms = list(algorithms or grids)
-    out = []
-    for pair in range(n_pairs):
-        for alg in algorithms:
-            for p in grid_cells(grids[alg]):
-                if n_fft is None or p["n_fft"] == n_fft:
-                    out.append((pair, alg, p))
-    return out
+    # one params dict per grid cell, shared by every pair (read-only): the
+    # engine recognises equal batch structures by params identity
+    cells = {alg: [p for p in grid_cells(grids[alg]) if n_fft is None or p["n_fft"] == n_fft]
+             for alg in algorithms}
+    return [(pair, alg, p) for pair in range(n_pairs) for alg in algorithms for p in cells[alg]]
 
 
 def frames(length, hop):
@@ -145,7 +143,8 @@ def engine_compute(clean, noisy, specs, ids, engine=None, align=True, stoi=True)
             nz = torch.as_tensor(np.stack([np.asarray(noisy[p], np.float64) for p in pairs])).cuda()
             cl = torch.as_tensor(np.stack([np.asarray(clean[p], np.float64) for p in pairs])).cuda()
             sub = [(slot[specs[ids[j]][0]], specs[ids[j]][1], specs[ids[j]][2]) for j in js]
-            res = eng.run(nz, sub, clean=cl, align=align, want_waveforms=stoi)
+            # batches of equal-length pairs over the same grid share one plan
+            res = eng.run(nz, sub, clean=cl, align=align, want_waveforms=stoi, reuse=True)
             cpow = np.array([float(np.dot(np.asarray(clean[p], np.float64),
                                           np.asarray(clean[p], np.float64))) for p in pairs])
             sig = np.array([s for (s, _, _) in sub], dtype=np.int64)
@@ -214,15 +213,19 @@ def select_best(specs, table, objective="snr", tol=None):
         groups.setdefault((pair, alg), []).append(cid)
     best = OrderedDict()
     for key, ids in groups.items():
-        incumbent, win = -1.0, -1
-        for cid in ids:
-            if not table[cid, 2]:
-                continue
-            s = table[cid, col]
-            if s != s:  # NaN
-                continue
-            if s > incumbent + tol:
-                incumbent, win = s, cid
+        ids = np.asarray(ids, dtype=np.int64)
+        sc = table[ids, col]
+        ok = (table[ids, 2] != 0) & (sc == sc)  # finite cell, score not NaN
+        sc = np.where(ok, sc, -np.inf)
+        # the scan's incumbent only ever increases: jump to the first cell
+        # after the current winner that beats it by more than tol
+        incumbent, win, start = -1.0, -1, 0
+        while start < len(ids):
+            hit = np.flatnonzero(sc[start:] > incumbent + tol)
+            if len(hit) == 0:
+                break
+            k = start + int(hit[0])
+            incumbent, win, start = float(sc[k]), int(ids[k]), k + 1
         best[key] = (win, incumbent if win >= 0 else None)
     return best
 

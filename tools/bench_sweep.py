@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--pairs", type=int, default=4)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--profile", action="store_true", help="cProfile the timed STOI sweeps (host side)")
     a = ap.parse_args()
     import torch
     pairs = [make_pair(200 + i, a.seconds) for i in range(a.pairs)]
@@ -43,11 +44,20 @@ def main():
         search.run_grid(clean, noisy, specs, compute=compute)  # warm-up
         torch.cuda.synchronize()
         ts = []
+        prof = None
+        if a.profile and stoi:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         for _ in range(a.reps):
             t0 = time.perf_counter()
             table, best = search.run_grid(clean, noisy, specs, compute=compute)
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
+        if prof is not None:
+            import pstats
+            prof.disable()
+            pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(30)
         key = "with_stoi" if stoi else "snr_only"
         out[key] = {"s_per_sweep": float(np.median(ts)), "cells_per_s": len(specs) / float(np.median(ts))}
         if stoi:
