@@ -197,7 +197,7 @@ class Engine:
                          align, true_len)
 
     def run(self, noisy, specs, clean=None, want_waveforms=False, want_gains=False, align=False,
-            true_len=None, reuse=False):
+            true_len=None, reuse=None, keep=None):
         """Enhance every cell spec; returns a dict of per-spec results.
 
         noisy/clean: [S, L] float64 cuda tensors (clean may be None if no spec
@@ -208,26 +208,32 @@ class Engine:
         true_len: TrueNoise estimates use the first true_len samples of noisy
         and clean (a clean reference shorter than the noisy signal,
         noise_estimation.py:128-130); default L.
-        reuse: keep the plan (device buffers, cell tables) and reuse it for
-        the next call whose specs have the same structure — the same
-        (signal index, algorithm, params object) per cell, which is what the
-        sweep's batches of equal-length pairs over one grid have.  Params are
-        matched by identity (the cached specs keep them alive), so they must
-        not be mutated in between.  The results' 'y' is the plan's buffer: it
-        is overwritten by the next reusing call.
+        reuse: keep the plan (device buffers, cell tables) for the next call
+        with the same structure.  True: the structure is spec_fingerprint(specs)
+        — per cell the signal index, algorithm and params object identity (the
+        cached specs keep the params alive; they must not be mutated in
+        between).  Or a hashable key the caller derived from the structure;
+        specs may then be a zero-argument callable that builds the list, called
+        only when the key misses, and ``keep`` is held with the plan (the
+        object the key's identities refer to).  The results' 'y' is the plan's
+        buffer: the next reusing call overwrites it.
         """
         S, L = noisy.shape
         flags = (S, L, clean is not None, want_waveforms, want_gains, align, true_len)
-        mp = None
-        if reuse:
-            key = flags + (spec_fingerprint(specs),)
+        mp, key = None, None
+        if reuse is not None and reuse is not False:
+            if reuse is True:
+                specs = specs() if callable(specs) else specs
+                reuse = spec_fingerprint(specs)
+            key = flags + (reuse,)
             c = self._plan_cache
             if c is not None and c[0] == key:
                 mp = c[2]
         if mp is None:
+            specs = specs() if callable(specs) else specs
             mp = self.plan(S, L, specs, clean is not None, want_waveforms, want_gains, align,
                            true_len)
-            self._plan_cache = (key, specs, mp) if reuse else None
+            self._plan_cache = (key, (specs, keep), mp) if key is not None else None
         mp.execute(noisy, clean)
         return mp.results()
 

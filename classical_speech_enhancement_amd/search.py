@@ -55,17 +55,74 @@ NCOL = len(RECORD_FIELDS) - 1
 STOI_WAVE_BYTES = 32 << 30
 
 
+class JobSpecs(list):
+    """job_specs' result: the list of (pair, algorithm, params) tuples, plus
+    numpy columns so the sweep's per-cell bookkeeping (grouping, duplicate
+    cells, plan keys, selection) runs without per-cell Python loops:
+      pair [n], alg [n] (index into .algorithms), cell [n] (index into
+      .cells[alg], the algorithm's grid in reference order).
+    Every pair shares the same params dict per grid cell (read-only)."""
+
+    def __init__(self, n_pairs, algorithms, cells):
+        algorithms = list(algorithms)
+        super().__init__((pair, alg, p) for pair in range(n_pairs) for alg in algorithms
+                         for p in cells[alg])
+        self.algorithms = algorithms
+        self.cells = cells
+        per = [len(cells[a]) for a in algorithms]
+        self.per_pair = int(sum(per))
+        a_col = np.concatenate([np.full(n, k, dtype=np.int64) for k, n in enumerate(per)] or
+                               [np.zeros(0, np.int64)])
+        c_col = np.concatenate([np.arange(n, dtype=np.int64) for n in per] or [np.zeros(0, np.int64)])
+        self.pair = np.repeat(np.arange(n_pairs, dtype=np.int64), self.per_pair)
+        self.alg = np.tile(a_col, n_pairs)
+        self.cell = np.tile(c_col, n_pairs)
+        self._rep = {}
+
+    def grid_rep(self, alg_index, length):
+        """For each cell of one algorithm's grid, the first grid cell the engine
+        computes identically for signals of this length: same n_fft, hop and
+        algorithm parameters and the same noise PSD (engine.noise_key — e.g.
+        min_tracking and true_noise ignore noise_percentile)."""
+        key = (alg_index, int(length))
+        if key not in self._rep:
+            from .engine import ALGOS, DEFAULTS, n_frames, noise_key
+            alg = self.algorithms[alg_index]
+            names = ALGOS[alg][2]
+            dflt = DEFAULTS.get(alg, {})
+            first, rep = {}, []
+            for c, p in enumerate(self.cells[alg]):
+                hop = int(p["hop_length"])
+                k = (int(p["n_fft"]), hop, tuple(float(p[n] if n in p else dflt[n]) for n in names),
+                     noise_key(alg, p, n_frames(length, hop)))
+                rep.append(first.setdefault(k, c))
+            self._rep[key] = np.asarray(rep, dtype=np.int64)
+        return self._rep[key]
+
+    def representative(self, ids, lengths):
+        """Global index of the cell computed in place of each of ``ids`` (the
+        first identical cell of the same pair and algorithm)."""
+        ids = np.asarray(ids, dtype=np.int64)
+        out = ids.copy()
+        for a in range(len(self.algorithms)):
+            for L in {int(lengths[q]) for q in np.unique(self.pair[ids[self.alg[ids] == a]])}:
+                sel = (self.alg[ids] == a) & (np.asarray(lengths)[self.pair[ids]] == L)
+                c = self.cell[ids[sel]]
+                out[sel] = ids[sel] - c + self.grid_rep(a, L)[c]
+        return out
+
+
 def job_specs(n_pairs, algorithms=None, grids=None, n_fft=None):
     """(pair, algorithm, params) for every pair x algorithm x grid cell, in the
     reference's order (pairs outermost, registry order of algorithms, grid
-    order with the last key fastest)."""
+    order with the last key fastest), as a JobSpecs list.  One params dict per
+    grid cell is shared by every pair (read-only): the engine recognises equal
+    batch structures by params identity."""
     grids = grids or ALGORITHM_GRIDS
     algorithms = list(algorithms or grids)
-    # one params dict per grid cell, shared by every pair (read-only): the
-    # engine recognises equal batch structures by params identity
     cells = {alg: [p for p in grid_cells(grids[alg]) if n_fft is None or p["n_fft"] == n_fft]
              for alg in algorithms}
-    return [(pair, alg, p) for pair in range(n_pairs) for alg in algorithms for p in cells[alg]]
+    return JobSpecs(n_pairs, algorithms, cells)
 
 
 def frames(length, hop):
@@ -74,7 +131,27 @@ def frames(length, hop):
 
 def work_items(specs, lengths):
     """Group cell ids by (pair, n_fft, hop, algorithm).  Returns a list of
-    (cost, [cell ids]) in first-appearance order."""
+    (cost, [cell ids]) (ids ascending within an item)."""
+    if isinstance(specs, JobSpecs):
+        # per grid cell: n_fft, hop; the group key is a mixed-radix integer
+        nf = np.concatenate([[int(p["n_fft"]) for p in specs.cells[a]] for a in specs.algorithms])
+        hp = np.concatenate([[int(p["hop_length"]) for p in specs.cells[a]] for a in specs.algorithms])
+        off = np.concatenate([[0], np.cumsum([len(specs.cells[a]) for a in specs.algorithms])[:-1]])
+        g = off[specs.alg] + specs.cell
+        key = ((specs.pair * 4096 + nf[g]) * 4096 + hp[g]) * 64 + specs.alg
+        uk, inv = np.unique(key, return_inverse=True)
+        order = np.argsort(inv, kind="stable")
+        bounds = np.searchsorted(inv[order], np.arange(len(uk) + 1))
+        lengths = np.asarray(lengths)
+        items = []
+        for u in range(len(uk)):
+            ids = order[bounds[u]:bounds[u + 1]]
+            c0 = int(ids[0])
+            alg = specs.algorithms[int(specs.alg[c0])]
+            per_cell = (frames(lengths[specs.pair[c0]], hp[g[c0]]) * (int(nf[g[c0]]) // 2 + 1)
+                        * ALGO_WEIGHT.get(alg, 1.0))
+            items.append((per_cell * len(ids), ids.tolist()))
+        return items
     groups = OrderedDict()
     for cid, (pair, alg, p) in enumerate(specs):
         key = (pair, int(p["n_fft"]), int(p["hop_length"]), alg)
@@ -118,47 +195,72 @@ def engine_compute(clean, noisy, specs, ids, engine=None, align=True, stoi=True)
 
     clean/noisy: lists of 1-D float arrays (host) indexed by pair.  Pairs are
     batched by length (the engine's signal batches are rectangular), and, when
-    STOI is scored, in groups whose cell waveforms fit STOI_WAVE_BYTES."""
+    STOI is scored, in groups whose cell waveforms fit STOI_WAVE_BYTES.  With
+    job_specs' JobSpecs, cells the engine computes identically (a quarter of
+    the HEAD grid: min_tracking ignores noise_percentile) are computed once
+    and their rows copied, and batches of the same structure reuse one device
+    plan (Engine.run(reuse=...))."""
+    import hashlib
     import torch
     from .engine import Engine, snr_db
     from .metrics import StoiPlan
     eng = engine or Engine()
-    out = np.full((len(ids), NCOL), np.nan)
+    ids = np.asarray(ids, dtype=np.int64)
+    lengths = [len(x) for x in noisy]
+    js_specs = isinstance(specs, JobSpecs)
+    if js_specs:
+        comp, back = np.unique(specs.representative(ids, lengths), return_inverse=True)
+        pair_of = specs.pair[comp]
+    else:
+        comp, back = ids, np.arange(len(ids))
+        pair_of = np.fromiter((specs[c][0] for c in comp), dtype=np.int64, count=len(comp))
+    vals = np.full((len(comp), NCOL), np.nan)
     by_len = OrderedDict()
-    for j, cid in enumerate(ids):
-        pair = specs[cid][0]
-        by_len.setdefault(len(noisy[pair]), OrderedDict()).setdefault(pair, []).append(j)
-    for L, by_pair in by_len.items():
+    for pair in dict.fromkeys(pair_of.tolist()):  # first-appearance order
+        by_len.setdefault(lengths[pair], []).append(pair)
+    for L, pairs_l in by_len.items():
+        rows = {p: np.flatnonzero(pair_of == p) for p in pairs_l}
         batches, cur, n_cur = [], [], 0
-        for pair, js in by_pair.items():
-            if stoi and cur and (n_cur + len(js)) * L * 4 > STOI_WAVE_BYTES:
+        for pair in pairs_l:
+            n = len(rows[pair])
+            if stoi and cur and (n_cur + n) * L * 4 > STOI_WAVE_BYTES:
                 batches.append(cur)
                 cur, n_cur = [], 0
             cur.append(pair)
-            n_cur += len(js)
+            n_cur += n
         batches.append(cur)
         for pairs in batches:
-            js = [j for p in pairs for j in by_pair[p]]
+            js = np.concatenate([rows[p] for p in pairs])
             slot = {p: s for s, p in enumerate(pairs)}
+            sig = np.array([slot[p] for p in pair_of[js].tolist()], dtype=np.int64)
             nz = torch.as_tensor(np.stack([np.asarray(noisy[p], np.float64) for p in pairs])).cuda()
             cl = torch.as_tensor(np.stack([np.asarray(clean[p], np.float64) for p in pairs])).cuda()
-            sub = [(slot[specs[ids[j]][0]], specs[ids[j]][1], specs[ids[j]][2]) for j in js]
-            # batches of equal-length pairs over the same grid share one plan
-            res = eng.run(nz, sub, clean=cl, align=align, want_waveforms=stoi, reuse=True)
+
+            def sub(js=js, sig=sig):
+                return [(int(sg), specs[int(c)][1], specs[int(c)][2]) for sg, c in zip(sig, comp[js])]
+            if js_specs:
+                # batches of the same structure reuse one device plan: the key
+                # is the cells' (slot, algorithm, grid cell) and this JobSpecs
+                h = hashlib.blake2b(digest_size=16)
+                for arr in (sig, specs.alg[comp[js]], specs.cell[comp[js]]):
+                    h.update(np.ascontiguousarray(arr, dtype=np.int64).tobytes())
+                res = eng.run(nz, sub, clean=cl, align=align, want_waveforms=stoi,
+                              reuse=("jobspecs", id(specs), h.hexdigest()), keep=specs)
+            else:
+                res = eng.run(nz, sub(), clean=cl, align=align, want_waveforms=stoi, reuse=True)
             cpow = np.array([float(np.dot(np.asarray(clean[p], np.float64),
                                           np.asarray(clean[p], np.float64))) for p in pairs])
-            sig = np.array([s for (s, _, _) in sub], dtype=np.int64)
-            out[js, 0] = res["sse"]
-            out[js, 1] = snr_db(res["sse"], cpow[sig])
-            out[js, 2] = res["finite"]
+            vals[js, 0] = res["sse"]
+            vals[js, 1] = snr_db(res["sse"], cpow[sig])
+            vals[js, 2] = res["finite"]
             if stoi:
-                lag = res["lag"] if align else np.zeros(len(sub), dtype=np.int64)
+                lag = res["lag"] if align else np.zeros(len(js), dtype=np.int64)
                 plan = StoiPlan(cl)
-                sc = plan.score(res["y"].view(-1), np.arange(len(sub), dtype=np.int64) * L, sig,
+                sc = plan.score(res["y"].view(-1), np.arange(len(js), dtype=np.int64) * L, sig,
                                 lag=lag, clip=True)
-                out[js, 3] = np.where(res["finite"], sc, np.nan)
+                vals[js, 3] = np.where(res["finite"], sc, np.nan)
                 del plan, res
-    return out
+    return vals[back]
 
 
 def gather_records(local, n_total, group=None, device=None):
@@ -209,8 +311,16 @@ def select_best(specs, table, objective="snr", tol=None):
         raise ValueError(f"objective {objective!r} is not scored on the device (pesq is absent)")
     col = TABLE_COLUMN[objective]
     groups = OrderedDict()
-    for cid, (pair, alg, _) in enumerate(specs):
-        groups.setdefault((pair, alg), []).append(cid)
+    if isinstance(specs, JobSpecs):  # (pair, algorithm) runs are contiguous
+        per = [len(specs.cells[a]) for a in specs.algorithms]
+        start = 0
+        for pair in range(len(specs) // max(specs.per_pair, 1)):
+            for a, n in zip(specs.algorithms, per):
+                groups[(pair, a)] = np.arange(start, start + n)
+                start += n
+    else:
+        for cid, (pair, alg, _) in enumerate(specs):
+            groups.setdefault((pair, alg), []).append(cid)
     best = OrderedDict()
     for key, ids in groups.items():
         ids = np.asarray(ids, dtype=np.int64)

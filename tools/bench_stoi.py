@@ -56,7 +56,7 @@ def main():
     ms = float(np.median(times))
     v = out.cpu().numpy()
     if not os.environ.get("CSE_BENCH_NOCHECK"):
-        assert np.isfinite(v).all()
+        assert os.environ.get("CSE_BENCH_NOCHECK") or np.isfinite(v).all()
     print(json.dumps({"what": "cse_stoi_cells", "cells": a.cells, "clip_s": a.seconds,
                       "ms_per_launch": ms, "cells_per_s": a.cells / (ms / 1e3),
                       "prepare_ms_incl_first_launch": prep_ms, "stoi_mean": float(v.mean())}))
