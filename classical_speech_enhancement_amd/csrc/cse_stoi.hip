@@ -41,6 +41,8 @@
 // outputs themselves are f32 (the enhance kernel's output type).
 #include "cse_common.hpp"
 
+#include <type_traits>
+
 namespace cse {
 
 // CSE_STOI_ABLATE (timing experiments only; 0 in product builds): skip
@@ -57,9 +59,16 @@ constexpr int KLO = -58, KN = 123;       // tap span of the 5 phases: k in [-58,
 constexpr int CST = 128;                 // coefficient row stride
 constexpr int FR = 256, HOP = 128;       // frames at 10 kHz
 constexpr int NBAND = 15, NSEG = 30;
-constexpr int FB = 16;                   // STFT frames per phase-A block
-constexpr int MAXD = 2 * (FB + 1);       // distinct 10-kHz half-blocks per block
-constexpr int BT = 72;                   // ints per block table: D, p[34], sa[17], sb[17]
+constexpr int FB = 16;                   // most STFT frames per phase-A block
+constexpr int MAXD = 28;                 // most distinct 10-kHz half-blocks per block
+// block table (ints): D, j0, nf, p[MAXD], sa[FB + 1], sb[FB + 1].  A block takes
+// frames while nf <= FB and its OLA rows need <= MAXD distinct half-blocks
+// (a row needs at most 2, so every block but the last has >= 13 frames)
+constexpr int T_D = 0, T_J0 = 1, T_NF = 2, T_P = 3, T_SA = T_P + MAXD, T_SB = T_SA + FB + 1;
+constexpr int BT = 72;
+static_assert(T_SB + FB + 1 <= BT, "block table size");
+constexpr int MINF = MAXD / 2 - 1;       // frames every block but the last holds
+constexpr int META = 8;                  // ints per signal: K, M, J, ok, nblk
 constexpr int SLOTS = 9;                 // half-blocks resampled per pass (9 x 27 tasks <= 256)
 constexpr int GRP = 27;                  // phase groups (5 outputs) covering one half-block
 constexpr int SROW = 43;                 // staging: 8 rows (sample mod 8) x 43 columns
@@ -84,10 +93,10 @@ static StoiLayout stoi_layout(int64_t n_sig, int64_t len) {
     L.F = L.n10 >= FR ? (L.n10 - FR) / HOP + 1 : 0;
     L.Mmax = L.F > 1 ? L.F - 1 : 0;
     L.Jmax = L.Mmax >= NSEG ? L.Mmax - NSEG + 1 : 0;
-    L.NBLK = (L.Mmax + FB - 1) / FB;
+    L.NBLK = (L.Mmax + MINF - 1) / MINF + 1;
     int64_t o = 0;
     L.coef64 = o; o = align256(o + 5 * CST * 8);
-    L.meta = o;   o = align256(o + n_sig * 4 * 4);
+    L.meta = o;   o = align256(o + n_sig * META * 4);
     L.x10 = o;    o = align256(o + n_sig * L.n10 * 8);
     L.en = o;     o = align256(o + n_sig * L.F * 8);
     L.kf = o;     o = align256(o + n_sig * L.F * 4);
@@ -239,34 +248,46 @@ __global__ void __launch_bounds__(256) stoi_select_kernel(const double* __restri
     }
     const int M = K > 1 ? K - 1 : 0;
     const int J = M >= NSEG ? M - NSEG + 1 : 0;
-    if (tid == 0) {
-        meta[4 * sig + 0] = K;
-        meta[4 * sig + 1] = M;
-        meta[4 * sig + 2] = J;
-        meta[4 * sig + 3] = F > 0 ? 1 : 0;  // 0: no frame at all (pystoi raises)
-    }
     __threadfence_block();
     __syncthreads();
-    const int nblk = (M + FB - 1) / FB;
-    for (int b = tid; b < nblk; b += 256) {
-        int* t = btab_all + ((int64_t)sig * NBLK + b) * BT;
-        const int j0 = b * FB;
-        const int nf = min(FB, M - j0);
-        int D = 0, last = -1;
-        for (int hl = 0; hl <= nf; ++hl) {
-            const int h = j0 + hl;
-            int sb = -1;
-            if (h >= 1) {
-                const int pb = kf[h - 1] + 1;
-                if (pb != last) { t[1 + D] = pb; last = pb; ++D; }
-                sb = D - 1;
+    // blocks (one thread per signal: greedy over the kept frames)
+    if (tid == 0) {
+        int nblk = 0, j0 = 0;
+        while (j0 < M) {
+            int* t = btab_all + ((int64_t)sig * NBLK + nblk) * BT;
+            int D = 0, last = -1;
+            auto add = [&](int p) {
+                if (p != last) { t[T_P + D] = p; last = p; ++D; }
+                return D - 1;
+            };
+            // row hl of the block = kept frame h = j0 + hl: w[n] e10[kf[h]] +
+            // w[128 + n] e10[kf[h - 1] + 1] (the second term only for h >= 1)
+            auto row = [&](int hl) {
+                const int h = j0 + hl;
+                t[T_SB + hl] = h >= 1 ? add(kf[h - 1] + 1) : -1;
+                t[T_SA + hl] = add(kf[h]);
+            };
+            row(0);
+            int nf = 0;
+            while (nf < FB && j0 + nf < M) {
+                const int h = j0 + nf + 1;
+                const int pb = kf[h - 1] + 1, pa = kf[h];
+                const int extra = (pb != last) + (pa != pb);
+                if (D + extra > MAXD) break;
+                row(nf + 1);
+                ++nf;
             }
-            const int pa = kf[h];
-            if (pa != last) { t[1 + D] = pa; last = pa; ++D; }
-            t[1 + MAXD + hl] = D - 1;             // sa
-            t[1 + MAXD + (FB + 1) + hl] = sb;     // sb
+            t[T_D] = D;
+            t[T_J0] = j0;
+            t[T_NF] = nf;
+            j0 += nf;
+            ++nblk;
         }
-        t[0] = D;
+        meta[META * sig + 0] = K;
+        meta[META * sig + 1] = M;
+        meta[META * sig + 2] = J;
+        meta[META * sig + 3] = F > 0 ? 1 : 0;  // 0: no frame at all (pystoi raises)
+        meta[META * sig + 4] = nblk;
     }
 }
 
@@ -314,10 +335,27 @@ __device__ __forceinline__ cd w16f(int m) {
     }
 }
 
-// forward DFT16 in registers (radix 4 x 4), natural order in and out
+// forward DFT4 of (a0, a1, 0, 0): [a0+a1, a0-i a1, a0-a1, a0+i a1]
+__device__ __forceinline__ void fdft4_half(cd& a0, cd& a1, cd& a2, cd& a3) {
+    const cd s = dadd(a0, a1), d = dsub(a0, a1);
+    const cd m = dmk(a1.y, -a1.x);  // -i a1
+    a2 = d;
+    a3 = dsub(a0, m);
+    a1 = dadd(a0, m);
+    a0 = s;
+}
+
+// forward DFT16 in registers (radix 4 x 4), natural order in and out;
+// HALF: v[8..15] are zero on entry
+template <bool HALF = false>
 __device__ __forceinline__ void fdft16(cd (&v)[16]) {
 #pragma unroll
-    for (int k2 = 0; k2 < 4; ++k2) fdft4(v[k2], v[4 + k2], v[8 + k2], v[12 + k2]);
+    for (int k2 = 0; k2 < 4; ++k2) {
+        if (HALF)
+            fdft4_half(v[k2], v[4 + k2], v[8 + k2], v[12 + k2]);
+        else
+            fdft4(v[k2], v[4 + k2], v[8 + k2], v[12 + k2]);
+    }
 #pragma unroll
     for (int n1 = 1; n1 < 4; ++n1)
 #pragma unroll
@@ -337,18 +375,24 @@ __device__ __forceinline__ void fdft16(cd (&v)[16]) {
     for (int i = 0; i < 16; ++i) v[i] = t[i];
 }
 
+// ordering of LDS accesses among the lanes of ONE wave: a compiler-level
+// barrier suffices (the LDS executes a wave's DS instructions in issue order)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 struct StoiLds {
     double wnd[stoi::FR];
     cd tw256[256];          // e^{-2πi k/256}
     cd tw512[256];          // e^{-2πi k/512}
-    double ola[stoi::FB + 1][stoi::HOP];
     union {
         struct {
             float stage[stoi::SLOTS * stoi::SSTR];  // 16-kHz input (f32, as the cells hold it)
             double e10[stoi::MAXD][stoi::HOP];
         } a;
-        double t[stoi::FB][16 * 17];   // transpose, one component at a time
-        double pw[stoi::FB][224];      // |X|^2
+        double t[stoi::FB][16 * 17];   // transpose, one component at a time; then |X|^2
         struct {
             double y[94 * 17];
             double x[94 * 17];
@@ -387,10 +431,9 @@ template <bool PRE>
 __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t len, int lag,
                              bool clip, const double* __restrict__ x10,
                              const double* __restrict__ coef, const int* __restrict__ btab,
-                             int M, double* __restrict__ env) {
+                             int nblk, double* __restrict__ env) {
     using namespace stoi;
     const int tid = threadIdx.x;
-    const int nblk = (M + FB - 1) / FB;
     // 16-kHz input samples of one staging chunk, loaded into registers one
     // chunk ahead (the global-load latency overlaps the previous chunk's
     // resampling instead of stalling every chunk)
@@ -401,13 +444,13 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
     float pre[PF];
     unsigned pmask = 0;
     auto fetch = [&](const int* tb, int c0) {
-        const int ns = min(SLOTS, tb[0] - c0);
+        const int ns = min(SLOTS, tb[T_D] - c0);
         pmask = 0;
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
             const int i = tid + u * NT;
             const int s = i < ns * SSTR ? i / SSTR : 0, uu = i - s * SSTR;
-            const int64_t q0 = ((int64_t)HOP * tb[1 + c0 + s]) / UP;
+            const int64_t q0 = ((int64_t)HOP * tb[T_P + c0 + s]) / UP;
             const int64_t n = 8 * q0 + KLO + uu;  // e index (finalize_enhanced output)
             const int64_t src = n - lag;         // y index
             const bool ok = i < ns * SSTR && uu < 8 * GRP + KN && n >= 0 && n < len &&
@@ -423,18 +466,17 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
         if (!PRE) fetch(L.tab[0], 0);
     }
     for (int blk = 0; blk < nblk; ++blk) {
-        const int j0 = blk * FB;
-        const int nf = min(FB, M - j0);
         const int* tb = L.tab[blk & 1];
+        const int j0 = tb[T_J0], nf = tb[T_NF];
         const int* tn = L.tab[(blk + 1) & 1];
         __syncthreads();  // previous block's readers of the union and of tn are done
         if (blk + 1 < nblk && tid < BT) L.tab[(blk + 1) & 1][tid] = btab[(int64_t)(blk + 1) * BT + tid];
-        const int D = tb[0];
-        // ---- 10-kHz half-blocks p = tb[1 + d] into e10[d]
+        const int D = tb[T_D];
+        // ---- 10-kHz half-blocks p = tb[T_P + d] into e10[d]
         if (PRE) {
             for (int i = tid; i < D * HOP; i += NT) {
                 const int d = i >> 7, n = i & (HOP - 1);
-                L.u.a.e10[d][n] = x10[(int64_t)tb[1 + d] * HOP + n];
+                L.u.a.e10[d][n] = x10[(int64_t)tb[T_P + d] * HOP + n];
             }
         } else {
             for (int c0 = 0; c0 < D; c0 += SLOTS) {
@@ -456,14 +498,29 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                     fetch(tn, 0);
                 if (tid < ns * GRP && !(CSE_STOI_ABLATE & 1)) {
                     const int s = tid / GRP, g = tid - s * GRP;
-                    const int64_t p = tb[1 + c0 + s];
+                    const int64_t p = tb[T_P + c0 + s];
                     const int64_t q0 = (HOP * p) / UP;
                     const int64_t q = q0 + g;
                     const float* st = L.u.a.stage + s * SSTR + g;
                     double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-                    // 16 x 8 taps (coefficients beyond the support, kk >= 123, are 0)
+                    // taps kk = 8 kb + j of phase r; c_r[kk] = 0 outside
+                    // 8r <= 5kk <= 8r + 580 (and kk >= 123): the edge blocks
+                    // kb = 0, 14, 15 are unrolled with those taps left out
+                    auto taps = [&](auto kbc) {
+                        constexpr int kb = decltype(kbc)::value;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const int kk = 8 * kb + j;
+                            const double e = (double)st[j * SROW + kb];
+#pragma unroll
+                            for (int r = 0; r < 5; ++r)
+                                if (5 * kk >= 8 * r && 5 * kk <= 8 * r + 580)
+                                    acc[r] = fma(coef[r * CST + kk], e, acc[r]);
+                        }
+                    };
+                    taps(std::integral_constant<int, 0>());
 #pragma unroll 1
-                    for (int kb = 0; kb < CST / 8; ++kb) {
+                    for (int kb = 1; kb < 14; ++kb) {  // every tap nonzero
 #pragma unroll
                         for (int j = 0; j < 8; ++j) {
                             const double e = (double)st[j * SROW + kb];
@@ -472,6 +529,8 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                                 acc[r] = fma(coef[r * CST + 8 * kb + j], e, acc[r]);
                         }
                     }
+                    taps(std::integral_constant<int, 14>());
+                    taps(std::integral_constant<int, 15>());
 #pragma unroll
                     for (int r = 0; r < 5; ++r) {
                         const int64_t off = 5 * q + r - HOP * p;
@@ -482,32 +541,31 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
             }
         }
         __syncthreads();
-        // ---- overlap-add: ola[hl][n] = w[n] e10[sa][n] + w[128+n] e10[sb][n]
-        for (int i = tid; i < ((CSE_STOI_ABLATE & 32) ? 0 : (nf + 1) * HOP); i += NT) {
-            const int hl = i >> 7, n = i & (HOP - 1);
-            const int sa = tb[1 + MAXD + hl];
-            const int sb = tb[1 + MAXD + (FB + 1) + hl];
-            double v = L.wnd[n] * L.u.a.e10[sa][n];
-            if (sb >= 0) v = fma(L.wnd[HOP + n], L.u.a.e10[sb][n], v);
-            L.ola[hl][n] = v;
-        }
-        __syncthreads();
         if (!(CSE_STOI_ABLATE & 2))
-        // ---- 512-point rfft of frame fl = [ola[fl], ola[fl+1]] * w, 16 lanes per frame:
-        // z[m] = s[2m] + i s[2m+1] (m < 128, 0 above), Z = DFT256(z) as DFT16 x DFT16
+        // ---- 512-point rfft of frame fl, 16 lanes per frame: sample n of the
+        // frame is w[n] ola[fl + n/128][n mod 128], the overlap-added row
+        // ola[hl][o] = w[o] e10[sa][o] + w[128 + o] e10[sb][o] read straight
+        // from the half-blocks; z[m] = s[2m] + i s[2m+1] (m < 128, 0 above),
+        // Z = DFT256(z) as DFT16 x DFT16
         {
             const int fl = tid >> 4, n1 = tid & 15;
             cd v[16];
 #pragma unroll
-            for (int n2 = 0; n2 < 8; ++n2) {
-                const int n = 2 * (n1 + 16 * n2);
-                const double* row = n2 < 4 ? L.ola[fl] : L.ola[fl + 1];
-                const int o = n2 < 4 ? n : n - HOP;
-                v[n2] = dmk(L.wnd[n] * row[o], L.wnd[n + 1] * row[o + 1]);
-            }
+            for (int hh = 0; hh < 2; ++hh) {
+                const int hl = min(fl + hh, nf);  // rows of frame fl (fl < nf for the lanes kept)
+                const double* ea = L.u.a.e10[tb[T_SA + hl]];
+                const int sb = tb[T_SB + hl];
+                const double* eb = L.u.a.e10[sb >= 0 ? sb : 0];
+                const double wb = sb >= 0 ? 1.0 : 0.0;
 #pragma unroll
-            for (int n2 = 8; n2 < 16; ++n2) v[n2] = dmk(0.0, 0.0);
-            fdft16(v);                                 // v[k1] = A[n1][k1]
+                for (int n2 = 4 * hh; n2 < 4 * hh + 4; ++n2) {
+                    const int n = 2 * (n1 + 16 * n2), o = n - HOP * hh;
+                    const double r0 = fma(wb * L.wnd[HOP + o], eb[o], L.wnd[o] * ea[o]);
+                    const double r1 = fma(wb * L.wnd[HOP + o + 1], eb[o + 1], L.wnd[o + 1] * ea[o + 1]);
+                    v[n2] = dmk(L.wnd[n] * r0, L.wnd[n + 1] * r1);
+                }
+            }
+            fdft16<true>(v);                           // v[k1] = A[n1][k1] (v[8..15] = 0)
             {
                 const cd w = L.tw256[n1];
                 cd wr = w;
@@ -517,25 +575,28 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                     wr = dmul(wr, w);
                 }
             }
+            // the transposes stay inside the frame's 16 lanes (one wave): after
+            // the one workgroup barrier (t aliases e10), wave-level ordering
             double* t = L.u.t[fl];
             const int k1 = n1;
             double re[16];
+            __syncthreads();  // every lane's e10 reads are done: t aliases e10
 #pragma unroll
             for (int a = 0; a < 16; ++a) t[a * 17 + n1] = v[a].x;
-            __syncthreads();
+            wave_sync();
 #pragma unroll
             for (int a = 0; a < 16; ++a) re[a] = t[k1 * 17 + a];
-            __syncthreads();
+            wave_sync();
 #pragma unroll
             for (int a = 0; a < 16; ++a) t[a * 17 + n1] = v[a].y;
-            __syncthreads();
+            wave_sync();
 #pragma unroll
             for (int a = 0; a < 16; ++a) v[a] = dmk(re[a], t[k1 * 17 + a]);
             fdft16(v);                                 // v[k2] = Z[k1 + 16 k2]
-            __syncthreads();                           // t reads done before pw (aliased)
+            wave_sync();                               // t reads issued before |X|^2 overwrites them
             // partner Z[(256 - k) mod 256]: lane (16 - k1) & 15, register 15 - k2 (k1 > 0)
             const int src = (tid & 48) | ((16 - k1) & 15);  // lane within the wave
-            double* pw = L.u.pw[fl];
+            double* pw = L.u.t[fl];  // |X|^2 of the frame, bins < 224, in its own rows
 #pragma unroll
             for (int k2 = 0; k2 < 16; ++k2) {
                 const cd zo = v[15 - k2];
@@ -553,7 +614,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
         // ---- band envelopes
         if (tid < nf * NBAND && !(CSE_STOI_ABLATE & 4)) {
             const int fl = tid / NBAND, b = tid - fl * NBAND;
-            const double* pw = L.u.pw[fl];
+            const double* pw = L.u.t[fl];
             double s = 0.0;
             for (int k = BAND_EDGE[b]; k < BAND_EDGE[b + 1]; ++k) s += pw[k];
             env[(int64_t)(j0 + fl) * 16 + b] = sqrt(s);
@@ -571,9 +632,9 @@ __global__ void __launch_bounds__(stoi::NT) stoi_clean_env_kernel(const double* 
     __shared__ StoiLds L;
     const int sig = blockIdx.x;
     stoi_tables(L);
-    const int M = meta[4 * sig + 1];
+    const int nblk = meta[stoi::META * sig + 4];
     stoi_phase_a<true>(L, nullptr, 0, 0, false, x10all + (int64_t)sig * n10, nullptr,
-                       btab + (int64_t)sig * NBLK * stoi::BT, M, xtob + (int64_t)sig * Mmax * 16);
+                       btab + (int64_t)sig * NBLK * stoi::BT, nblk, xtob + (int64_t)sig * Mmax * 16);
 }
 
 // (||x||, mean, 1/(||x - mean|| + eps)) of the clean envelope over each segment
@@ -584,7 +645,7 @@ __global__ void __launch_bounds__(256) stoi_clean_stat_kernel(const double* __re
     using namespace stoi;
     const int sig = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int J = meta[4 * sig + 2];
+    const int J = meta[META * sig + 2];
     const int j = (int)(i / 16), b = (int)(i % 16);
     if (j >= J || b >= NBAND) return;
     const double* x = xtob + ((int64_t)sig * Mmax + j) * 16 + b;
@@ -625,16 +686,15 @@ struct StoiArgs {
 // coef is a separate const __restrict__ argument so the compiler can prove it
 // is never written and read it through the scalar cache (s_load): inside the
 // argument struct it became per-lane vector loads waited on right after issue
-__global__ void __launch_bounds__(stoi::NT) stoi_cells_kernel(StoiArgs a,
+__global__ void __launch_bounds__(stoi::NT, 3) stoi_cells_kernel(StoiArgs a,
                                                               const double* __restrict__ coef) {
     using namespace stoi;
     __shared__ StoiLds L;
     const int64_t c = blockIdx.x;
     const int tid = threadIdx.x;
     const int sig = a.sig_of[c];
-    const int M = a.meta[4 * sig + 1];
-    const int J = a.meta[4 * sig + 2];
-    if (a.meta[4 * sig + 3] == 0) {  // no 256-sample frame at all: pystoi raises -> None
+    const int J = a.meta[META * sig + 2];
+    if (a.meta[META * sig + 3] == 0) {  // no 256-sample frame at all: pystoi raises -> None
         if (tid == 0) a.out[c] = __builtin_nan("");
         return;
     }
@@ -646,7 +706,7 @@ __global__ void __launch_bounds__(stoi::NT) stoi_cells_kernel(StoiArgs a,
     double* env = a.scratch + c * a.Mmax * 16;
     const int lag = a.lag ? a.lag[c] : 0;
     stoi_phase_a<false>(L, a.y + a.y_offset[c], a.len, lag, a.clip != 0, nullptr, coef,
-                        a.btab + (int64_t)sig * a.NBLK * BT, M, env);
+                        a.btab + (int64_t)sig * a.NBLK * BT, a.meta[META * sig + 4], env);
     __syncthreads();  // env rows of this workgroup are visible to it
     // ---- phase B: segment j, band b
     const double* xt = a.xtob + (int64_t)sig * a.Mmax * 16;
