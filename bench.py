@@ -167,9 +167,10 @@ def cpu_run(budget_s, seconds, n_fft, y_cells, timed=True):
     return base, snr, ys
 
 
-def load_pmc(units_per_launch):
-    """Counters of the enhance kernel for this exact launch size, from the
-    committed rocprofv3 PMC passes (profiles/pmc_*.json, tools/pmc_summary.py)."""
+def load_pmc(units_per_launch, n_fft):
+    """Counters of the enhance kernel for this exact launch size and n_fft,
+    from the committed rocprofv3 PMC passes (profiles/pmc_*.json,
+    tools/pmc_summary.py; the newest round wins)."""
     import glob
     best = None
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
@@ -177,7 +178,8 @@ def load_pmc(units_per_launch):
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("units_per_launch") == units_per_launch:
+        if (d.get("units_per_launch") == units_per_launch and f"<{n_fft}" in d.get("kernel", "")
+                and (best is None or str(d.get("round", "")) >= str(best.get("round", "")))):
             best = d
     return best
 
@@ -340,7 +342,7 @@ def main():
     value = total_units * args.steps / dt
     bytes_per_unit = 12 * (args.nfft // 2 + 1)
     achieved = units * bytes_per_unit / (kern_ms / 1e3)
-    pmc = load_pmc(units)
+    pmc = load_pmc(units, args.nfft)
     roof = {
         "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
         "frac": achieved / HBM_PEAK, "traffic": None,
@@ -359,10 +361,11 @@ def main():
                  "frac_at_2p4ghz": need / (SIMDS * CLOCK * kern_ms / 1e3),
                  "cycles_per": f"VALU {VALU_CYC}, transcendental {TRANS_CYC} per wave64 per SIMD",
                  "source": pmc.get("source")}
-            gui = pmc.get("grbm_gui_active")
-            if gui:  # the clock the chip held during the profiled launch (DVFS)
-                v["clock_ghz"] = gui / 8 / (pmc["kernel_ms"] / 1e3) / 1e9
-                v["frac"] = need / (SIMDS * gui / 8)
+            busy = pmc.get("sq_busy_cycles")
+            if busy:  # per-SE cycles with waves resident (summed over 32 SEs): the clock held
+                cyc = busy / 32
+                v["clock_ghz"] = cyc / (pmc["kernel_ms"] / 1e3) / 1e9
+                v["frac"] = need / (SIMDS * cyc)
             roof["valu"] = v
     res = {
         "metric": METRIC,

@@ -5,8 +5,10 @@ and calls, and the PMC counters of the separate --pmc passes, per launch
 (counter sum over the profiled launches / launches).  HBM traffic per launch =
 (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 (gfx950 correction, MI355X_MICROARCH.md
 HBM/rocprofv3 section: FETCH_SIZE counts half the bytes of wide streaming reads).
-VALU issue fraction = (2 x (VALU - TRANS) + 8 x TRANS) SIMD cycles over
-1024 SIMDs x GRBM_GUI_ACTIVE / 8 (rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs).
+VALU issue fraction = (2 x (VALU - TRANS) + 8 x TRANS) SIMD cycles (fp64 FMA/MUL/ADD
+at 4) over 1024 SIMDs x SQ_BUSY_CYCLES / 32 (per-shader-engine cycles with
+waves resident, summed over the 32 SEs).  GRBM_GUI_ACTIVE / 8 read twice the
+shader clock on the r02 boxes, so it is only recorded.
 
     python tools/pmc_summary.py TAG ROUND [UNITS_512 UNITS_1024]
 
@@ -51,12 +53,17 @@ def derive(pmc, kernel_ms):
     d = {}
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         d["hbm_bytes_per_launch"] = (2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024
-    vi, tr, gui = pmc.get("SQ_INSTS_VALU"), pmc.get("SQ_INSTS_VALU_TRANS_F32", 0.0), pmc.get("GRBM_GUI_ACTIVE")
-    if vi and gui:
-        need = VALU_CYC * (vi - tr) + TRANS_CYC * tr
+    vi, tr = pmc.get("SQ_INSTS_VALU"), pmc.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
+    f64 = sum(pmc.get(k, 0.0) for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
+                                         "SQ_INSTS_VALU_ADD_F64"))
+    busy = pmc.get("SQ_BUSY_CYCLES")
+    if vi and busy:
+        need = VALU_CYC * (vi - tr - f64) + TRANS_CYC * tr + 2 * VALU_CYC * f64
+        cyc = busy / 32
         d["valu_issue_cycles"] = need
-        d["valu_frac"] = need / (SIMDS * gui / 8)
-        d["clock_ghz_profiled"] = gui / 8 / (kernel_ms / 1e3) / 1e9 if kernel_ms else None
+        d["busy_cycles_per_se"] = cyc
+        d["valu_frac"] = need / (SIMDS * cyc)
+        d["clock_ghz_profiled"] = cyc / (kernel_ms / 1e3) / 1e9 if kernel_ms else None
     if "SQ_WAVE_CYCLES" in pmc:
         w = pmc["SQ_WAVE_CYCLES"]
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
@@ -104,7 +111,8 @@ def main(tag, rnd, units512=None, units1024=None):
                "hbm_bytes_per_launch": k.get("hbm_bytes_per_launch"),
                "sq_insts_valu": pmc.get("SQ_INSTS_VALU"), "sq_insts_valu_trans": pmc.get("SQ_INSTS_VALU_TRANS_F32"),
                "grbm_gui_active": pmc.get("GRBM_GUI_ACTIVE"),
-               "valu_frac": k.get("valu_frac"),
+               "sq_busy_cycles": pmc.get("SQ_BUSY_CYCLES"),
+               "valu_frac": k.get("valu_frac"), "clock_ghz_profiled": k.get("clock_ghz_profiled"),
                "source": f"profiles/{rnd}_kernels.json (tools/profile_all.sh {tag})"}
         json.dump(out, open(os.path.join(REPO, "profiles", f"pmc_{key}_{rnd}.json"), "w"), indent=1)
     for key, k in summary["kernels"].items():
