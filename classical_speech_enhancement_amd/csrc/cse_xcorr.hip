@@ -32,49 +32,68 @@ constexpr int XH = XN / 2;    // complex FFT length
 constexpr int XB = XN - 2 * 1600;  // output samples per block: the 0.1-s lags of 16 kHz fill XN
 constexpr int XT = 256;       // threads per workgroup
 constexpr int XCAND = 64;     // candidates re-evaluated in fp64
+constexpr int XHP = XH + XH / 16;  // LDS FFT buffer, one pad slot after every 16 points
+// padded LDS index: the first Stockham pass stores 16 consecutive points per
+// lane (lane stride 16 x 8 B, a 32-way bank conflict unpadded; 17 x 8 B with
+// the pad), every other access runs over consecutive points
+__device__ __forceinline__ int px(int p) { return p + (p >> 4); }
 #ifndef CSE_XC_WG_PER_CU
 #define CSE_XC_WG_PER_CU 3    // 168 VGPRs + 72 B spill: 4% faster than 2 (192, no spill); 4 spills 240 B
 #endif
 
+// one radix-16 Stockham pass of stride NS (compile-time, so every padded
+// address is a constant offset from one per-lane base)
+template <int DIR, int NS>
+__device__ __forceinline__ void fft4096_pass(cf* buf) {
+    const int j = threadIdx.x;
+    cf v[16];
+    const int pj = px(j);  // point j + 256 r sits at pj + 272 r
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = buf[pj + r * (XH / 16 + XH / 256)];
+    const int k = j % NS;
+    if (NS > 1) {
+        // w^r, w = e^{DIR 2πi k/(16 NS)}: one accurate sincos, then a product
+        // chain (|error| <= 15 ulp, far inside the candidate margin)
+        // (the argument is hidden from the optimiser: hoisting the chain out of
+        // the block loop would pin 2 x 30 VGPRs)
+        float s, c, arg = (float)(DIR * 2 * k) / (float)(NS * 16);
+        asm volatile("" : "+v"(arg));
+        sincospif(arg, &s, &c);
+        const cf w = cmk(c, s);
+        cf wr = w;
+#pragma unroll
+        for (int r = 1; r < 16; ++r) {
+            v[r] = cmul(v[r], wr);
+            wr = cmul(wr, w);
+        }
+    }
+    if (DIR > 0) {
+        idft16(v);
+    } else {  // forward = conj(inverse(conj(v)))
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r].y = -v[r].y;
+        idft16(v);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r].y = -v[r].y;
+    }
+    __syncthreads();
+    // px(base + r NS) = px(base) + r (NS + NS / 16) for NS >= 16 (base + r NS never
+    // carries into the pad index); NS = 1: base = 16 j, px = 17 j + r
+    const int base = (j / NS) * NS * 16 + k;
+    const int pb = px(base);
+    constexpr int PS = NS == 1 ? 1 : NS + NS / 16;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) buf[pb + r * PS] = v[r];
+    __syncthreads();
+}
+
 // forward (DIR = -1) / inverse (DIR = +1, unnormalised) 4096-point FFT in LDS,
 // radix-16 Stockham (Govindaraju et al. 2008 form): 3 passes, natural order out
 template <int DIR>
-__device__ void fft4096(cf* buf) {
-    const int j = threadIdx.x;
-#pragma unroll 1
-    for (int ns = 1; ns < XH; ns *= 16) {
-        cf v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = buf[j + r * (XH / 16)];
-        const int k = j % ns;
-        if (ns > 1) {
-            // w^r, w = e^{DIR 2πi k/(16 ns)}: one accurate sincos, then a product
-            // chain (|error| <= 15 ulp, far inside the candidate margin)
-            float s, c;
-            sincospif((float)(DIR * 2 * k) / (float)(ns * 16), &s, &c);
-            const cf w = cmk(c, s);
-            cf wr = w;
-#pragma unroll
-            for (int r = 1; r < 16; ++r) {
-                v[r] = cmul(v[r], wr);
-                wr = cmul(wr, w);
-            }
-        }
-        if (DIR > 0) {
-            idft16(v);
-        } else {  // forward = conj(inverse(conj(v)))
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[r].y = -v[r].y;
-            idft16(v);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[r].y = -v[r].y;
-        }
-        __syncthreads();
-        const int base = (j / ns) * ns * 16 + k;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) buf[base + r * ns] = v[r];
-        __syncthreads();
-    }
+__device__ __forceinline__ void fft4096(cf* buf) {
+    fft4096_pass<DIR, 1>(buf);
+    fft4096_pass<DIR, 16>(buf);
+    fft4096_pass<DIR, 256>(buf);
 }
 
 // X(f), f = 0..XH, of the real sequence x[2m] + i x[2m+1] = buf[m] after fft4096<-1>:
@@ -82,18 +101,50 @@ __device__ void fft4096(cf* buf) {
 // tw = e^{-2πi f/XN} is passed in (thread-owned bins f = tid + 256 r share
 // e^{-2πi tid/XN} and differ by the compile-time rotor e^{-2πi r/32})
 __device__ __forceinline__ cf rfft_bin(const cf* buf, int f, cf tw) {
-    if (f == XH) return cmk(buf[0].x - buf[0].y, 0.0f);
-    const cf z = buf[f];
-    const cf w = buf[(XH - f) & (XH - 1)];
+    if (f == XH) return cmk(buf[0].x - buf[0].y, 0.0f);  // px(0) = 0
+    const cf z = buf[px(f)];
+    const cf w = buf[px((XH - f) & (XH - 1))];
     const cf e = cmk(0.5f * (z.x + w.x), 0.5f * (z.y - w.y));
     const cf o = cmk(0.5f * (z.y + w.y), -0.5f * (z.x - w.x));
     return cadd(e, cmul(tw, o));
+}
+
+// the same from the two loaded points z = Z_f, w = Z_{(XH - f) mod XH}
+__device__ __forceinline__ cf rfft_pair(cf z, cf w, cf tw) {
+    const cf e = cmk(0.5f * (z.x + w.x), 0.5f * (z.y - w.y));
+    const cf o = cmk(0.5f * (z.y + w.y), -0.5f * (z.x - w.x));
+    return cadd(e, cmul(tw, o));
+}
+
+// padded LDS index of the mirror (XH - f) mod XH of the lane's bin f = t + 256 r:
+// t > 0: (256 - t) + 256 (15 - r); t = 0: 256 (16 - r) mod XH.  mirror_base(t)
+// + 272 (15 - r) covers both, except (t, r) = (0, 0) -> 0 (see mirror_at)
+__device__ __forceinline__ int mirror_base(int t) { return t == 0 ? 272 : px(256 - t); }
+__device__ __forceinline__ int mirror_at(int mb, int t, int r) {
+    const int q = mb + 272 * (15 - r);
+    return r == 0 ? (t == 0 ? 0 : q) : q;
 }
 
 __device__ __forceinline__ cf bin_rotor(int f) {
     float s, c;
     sincospif(-(float)(2 * f) / (float)XN, &s, &c);
     return cmk(c, s);
+}
+
+// per-lane sum of ld(q), q = tid, tid + XT, ... < n, in ascending q, with 8 loads
+// in flight (a plain strided loop waits out one memory latency per element)
+template <typename Load>
+__device__ __forceinline__ double strided_sum8(int n, Load ld) {
+    double acc = 0.0;
+    for (int q = threadIdx.x; q < n; q += 8 * XT) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ld(min(q + u * XT, n - 1));
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (q + u * XT < n) acc += v[u];
+    }
+    return acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -107,13 +158,12 @@ __global__ void __launch_bounds__(XT) xcorr_prep_kernel(const double* __restrict
                                                          double* __restrict__ W,
                                                          double* __restrict__ Z,
                                                          double* __restrict__ rnorm) {
-    __shared__ cf buf[XH];
+    __shared__ cf buf[XHP];
     __shared__ double red[XT];
     const int sig = blockIdx.y, tid = threadIdx.x;
     const double* c = clean + (int64_t)sig * len;
     // mean of clean[0, n)
-    double acc = 0.0;
-    for (int q = tid; q < n; q += XT) acc += c[q];
+    const double acc = strided_sum8(n, [&](int q) { return c[q]; });
     red[tid] = acc;
     __syncthreads();
     for (int s = XT / 2; s > 0; s >>= 1) {
@@ -125,15 +175,24 @@ __global__ void __launch_bounds__(XT) xcorr_prep_kernel(const double* __restrict
     const int b = blockIdx.x;
     if (b < nb) {
         // window r0[b XB - max_lag + v], v < XB + 2 max_lag, zero elsewhere
-        for (int m = tid; m < XH; m += XT) {
-            float xv[2];
+        // (all 32 loads of a lane issued before the first use; clamped indices)
+        double xv[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+            const int v = 2 * tid + (u & 1) + 2 * XT * (u >> 1);
+            const int q = b * XB - max_lag + v;
+            xv[u] = c[min(max(q, 0), n - 1)];
+        }
+#pragma unroll
+        for (int u = 0; u < 32; u += 2) {
+            float x2[2];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                const int v = 2 * m + e;
+                const int v = 2 * tid + e + 2 * XT * (u >> 1);
                 const int q = b * XB - max_lag + v;
-                xv[e] = (v < XB + 2 * max_lag && q >= 0 && q < n) ? (float)(c[q] - mu) : 0.0f;
+                x2[e] = (v < XB + 2 * max_lag && q >= 0 && q < n) ? (float)(xv[u + e] - mu) : 0.0f;
             }
-            buf[m] = cmk(xv[0], xv[1]);
+            buf[px(tid + XT * (u >> 1))] = cmk(x2[0], x2[1]);
         }
         __syncthreads();
         fft4096<-1>(buf);
@@ -144,13 +203,20 @@ __global__ void __launch_bounds__(XT) xcorr_prep_kernel(const double* __restrict
         }
         return;
     }
-    // block nb: fp64 tables (serial prefix sums are short: <= max_lag terms each side)
+    // block nb: fp64 tables r0, ||r0||^2, W, Z
     double* r0 = r0buf + (int64_t)sig * n;
-    double sq = 0.0;
-    for (int q = tid; q < n; q += XT) {
-        const double v = c[q] - mu;
-        r0[q] = v;
-        sq += v * v;
+    double sq = 0.0, tp = 0.0;  // ||r0||^2 and sum(r0) partials
+    for (int q = tid; q < n; q += 8 * XT) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = c[min(q + u * XT, n - 1)] - mu;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (q + u * XT < n) {
+                r0[q + u * XT] = v[u];
+                sq += v[u] * v[u];
+                tp += v[u];
+            }
     }
     red[tid] = sq;
     __syncthreads();
@@ -160,32 +226,58 @@ __global__ void __launch_bounds__(XT) xcorr_prep_kernel(const double* __restrict
     }
     const double r2 = red[0];
     __syncthreads();
-    double tp = 0.0;
-    for (int q = tid; q < n; q += XT) tp += r0[q];
     red[tid] = tp;
     __syncthreads();
     for (int s = XT / 2; s > 0; s >>= 1) {
         if (tid < s) red[tid] += red[tid + s];
         __syncthreads();
     }
+    const double total = red[0];
+    if (tid == 0) rnorm[sig] = r2;
+    // W(l) = total - sum_{q < l} r0[q], W(-l) = total - sum_{q >= n - l} r0[q] and
+    // Z(+-l) = the clean energy of the l padded head / tail samples, l = 1..max_lag:
+    // four prefix sums, a chunk of CH lags per lane plus a block scan of the chunk
+    // sums (a single lane walking max_lag dependent steps took ~0.3 ms)
+    double* sc = (double*)buf;  // 4 x XT scan slots in the idle FFT buffer
+    const int CH = (max_lag + XT - 1) / XT;
+    const int l0 = tid * CH + 1, l1 = min(l0 + CH - 1, max_lag);
+    double p[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int l = l0; l <= l1; ++l) {
+        p[0] += c[l - 1] - mu;  // = r0[l - 1]
+        p[1] += c[n - l] - mu;
+        p[2] += c[l - 1] * c[l - 1];
+        p[3] += c[len - l] * c[len - l];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sc[k * XT + tid] = p[k];
+    __syncthreads();
+    for (int off = 1; off < XT; off <<= 1) {  // inclusive Hillis-Steele scan
+        double t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = tid >= off ? sc[k * XT + tid - off] : 0.0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sc[k * XT + tid] += t[k];
+        __syncthreads();
+    }
+    double run[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) run[k] = sc[k * XT + tid] - p[k];  // exclusive
+    double* w = W + (int64_t)sig * (2 * max_lag + 1) + max_lag;
+    double* z = Z + (int64_t)sig * (2 * max_lag + 1) + max_lag;
     if (tid == 0) {
-        rnorm[sig] = r2;
-        const double total = red[0];
-        double* w = W + (int64_t)sig * (2 * max_lag + 1) + max_lag;
-        double* z = Z + (int64_t)sig * (2 * max_lag + 1) + max_lag;
         w[0] = total;
         z[0] = 0.0;
-        double head = 0.0, tail = 0.0, zh = 0.0, zt = 0.0;
-        for (int l = 1; l <= max_lag; ++l) {
-            head += r0[l - 1];  // sum_{q < l} r0[q]
-            tail += r0[n - l];  // sum_{q >= n - l} r0[q]
-            w[l] = total - head;
-            w[-l] = total - tail;
-            zh += c[l - 1] * c[l - 1];              // clean energy of the l padded head samples
-            zt += c[len - l] * c[len - l];          // ... of the l padded tail samples
-            z[l] = zh;
-            z[-l] = zt;
-        }
+    }
+    for (int l = l0; l <= l1; ++l) {
+        run[0] += c[l - 1] - mu;
+        run[1] += c[n - l] - mu;
+        run[2] += c[l - 1] * c[l - 1];
+        run[3] += c[len - l] * c[len - l];
+        w[l] = total - run[0];
+        w[-l] = total - run[1];
+        z[l] = run[2];
+        z[-l] = run[3];
     }
 }
 
@@ -221,7 +313,7 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 }
 
 __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs a) {
-    __shared__ cf buf[XH];
+    __shared__ cf buf[XHP];
     __shared__ double red[XT];
     __shared__ float rv[XT];
     __shared__ int ri[XT];
@@ -232,12 +324,67 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     const float* e = a.head + a.head_offset[cell];
     const int n = a.n, L = a.max_lag;
 
-    // mean and energy of e[0, n)
+    // C(f) = sum_b R_b(f) conj(S_b(f)); thread owns f = tid + XT r (+ f = XH on thread 0).
+    // The blocks tile e[0, n) exactly once, so the mean and energy of e are
+    // accumulated from the same loads (all 32 of a block's samples per lane are
+    // issued before the first is used: one memory latency per block, not 16).
+    cf C[16];
+    cf Cn = cmk(0.0f, 0.0f);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) C[r] = cmk(0.0f, 0.0f);
     double s1 = 0.0, s2 = 0.0;
-    for (int m = tid; m < n; m += XT) {
-        const double v = e[m];
-        s1 += v;
-        s2 += v * v;
+    const float2* Rs = a.R + (int64_t)sig * a.nb * (XH + 1);
+    const cf rot_tid = bin_rotor(tid);
+    const int pt = px(tid), mb = mirror_base(tid);
+    // raw buffer over e[0, n): out-of-range loads return 0 (CDNA buffer
+    // resource, word 3 = 0x00020000: 32-bit data format, no swizzle)
+    const __amdgpu_buffer_rsrc_t erc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)e, (short)0, 4 * n, 0x00020000);
+#pragma unroll 1
+    for (int b = 0; b < a.nb; ++b) {
+        // samples v = 2 tid + (u & 1) + 512 (u >> 1) of the block; v < XB needs
+        // u >> 1 <= 9 (and tid < 192 at 9); q >= n reads 0 (buffer range check)
+        float x[20];
+#pragma unroll
+        for (int u = 0; u < 20; ++u) {
+            const int v = 2 * tid + (u & 1) + 2 * XT * (u >> 1);
+            const float t = __builtin_bit_cast(  // the builtin returns the raw 32 bits
+                float, __builtin_amdgcn_raw_buffer_load_b32(erc, 4 * (b * XB + v), 0, 0));
+            x[u] = (u < 18 || v < XB) ? t : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 20; ++u) {
+            s1 += (double)x[u];
+            s2 += (double)x[u] * (double)x[u];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            buf[pt + 272 * r] = r < 10 ? cmk(x[2 * r], x[2 * r + 1]) : cmk(0.0f, 0.0f);
+        // R_b is issued before the transform and consumed after it
+        const float2* Rb = Rs + (int64_t)b * (XH + 1);
+        float2 rr[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) rr[r] = Rb[tid + XT * r];
+        __syncthreads();
+        fft4096<-1>(buf);
+        cf rt = rot_tid;  // hidden: the 16 derived rotors must not live across the FFT
+        asm volatile("" : "+v"(rt.x), "+v"(rt.y));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            // e^{-2πi (tid + 256 r)/8192} = rot_tid * e^{-2πi r/32}
+            const cf s = rfft_pair(buf[pt + 272 * r], buf[mirror_at(mb, tid, r)],
+                                   cmul(rt, cmk(Rot32::c[r], -Rot32::s[r])));
+            // R conj(S)
+            C[r].x += rr[r].x * s.x + rr[r].y * s.y;
+            C[r].y += rr[r].y * s.x - rr[r].x * s.y;
+        }
+        if (tid == 0) {
+            const cf s = rfft_bin(buf, XH, cmk(1.0f, 0.0f));
+            const float2 rr = Rb[XH];
+            Cn.x += rr.x * s.x + rr.y * s.y;
+            Cn.y += rr.y * s.x - rr.x * s.y;
+        }
+        __syncthreads();
     }
     s1 = block_sum(s1, red);
     s2 = block_sum(s2, red);
@@ -251,46 +398,9 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     }
     const double mu = s1 / n;
     const double snorm = fmax(s2 - n * mu * mu, 0.0);
-
-    // C(f) = sum_b R_b(f) conj(S_b(f)); thread owns f = tid + XT r (+ f = XH on thread 0)
-    cf C[16];
-    cf Cn = cmk(0.0f, 0.0f);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) C[r] = cmk(0.0f, 0.0f);
-    const float2* Rs = a.R + (int64_t)sig * a.nb * (XH + 1);
-    const cf rot_tid = bin_rotor(tid);
-#pragma unroll 1
-    for (int b = 0; b < a.nb; ++b) {
-        for (int m = tid; m < XH; m += XT) {
-            const int q0 = b * XB + 2 * m;
-            const float x0 = (2 * m < XB && q0 < n) ? e[q0] : 0.0f;
-            const float x1 = (2 * m + 1 < XB && q0 + 1 < n) ? e[q0 + 1] : 0.0f;
-            buf[m] = cmk(x0, x1);
-        }
-        __syncthreads();
-        fft4096<-1>(buf);
-        const float2* Rb = Rs + (int64_t)b * (XH + 1);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int f = tid + XT * r;
-            // e^{-2πi (tid + 256 r)/8192} = rot_tid * e^{-2πi r/32}
-            const cf s = rfft_bin(buf, f, cmul(rot_tid, cmk(Rot32::c[r], -Rot32::s[r])));
-            const float2 rr = Rb[f];
-            // R conj(S)
-            C[r].x += rr.x * s.x + rr.y * s.y;
-            C[r].y += rr.y * s.x - rr.x * s.y;
-        }
-        if (tid == 0) {
-            const cf s = rfft_bin(buf, XH, cmk(1.0f, 0.0f));
-            const float2 rr = Rb[XH];
-            Cn.x += rr.x * s.x + rr.y * s.y;
-            Cn.y += rr.y * s.x - rr.x * s.y;
-        }
-        __syncthreads();
-    }
     // inverse real transform: Zi(f) = (C_f + conj C_{XH-f}) + i e^{+2πi f/XN} (C_f - conj C_{XH-f})
 #pragma unroll
-    for (int r = 0; r < 16; ++r) buf[tid + XT * r] = C[r];
+    for (int r = 0; r < 16; ++r) buf[pt + 272 * r] = C[r];
     __shared__ cf cnyq;
     if (tid == 0) cnyq = Cn;
     __syncthreads();
@@ -298,7 +408,7 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     for (int r = 0; r < 16; ++r) {
         const int f = tid + XT * r;
         const cf cf_ = C[r];
-        const cf cm = (f == 0) ? cnyq : buf[XH - f];
+        const cf cm = (f == 0) ? cnyq : buf[mirror_at(mb, tid, r)];
         const cf ev = cmk(cf_.x + cm.x, cf_.y - cm.y);
         const cf od = cmk(cf_.x - cm.x, cf_.y + cm.y);
         const cf tw = cmul(rot_tid, cmk(Rot32::c[r], -Rot32::s[r]));  // e^{-2πi f/XN}
@@ -307,7 +417,7 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) buf[tid + XT * r] = C[r];
+    for (int r = 0; r < 16; ++r) buf[pt + 272 * r] = C[r];
     __syncthreads();
     fft4096<1>(buf);
 
@@ -316,7 +426,7 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     float best = -INFINITY;
     int bi = 0x7fffffff;
     for (int k = tid; k <= 2 * L; k += XT) {
-        const cf z = buf[k >> 1];
+        const cf z = buf[px(k >> 1)];
         const float craw = ((k & 1) ? z.y : z.x) * (1.0f / XN);
         const float v = craw - (float)(mu * Ws[k]);
         if (a.corr) a.corr[(int64_t)cell * (2 * L + 1) + k] = v;
@@ -345,7 +455,7 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     if (tid == 0) ncand = 0;
     __syncthreads();
     for (int k = tid; k <= 2 * L; k += XT) {
-        const cf z = buf[k >> 1];
+        const cf z = buf[px(k >> 1)];
         const float v = ((k & 1) ? z.y : z.x) * (1.0f / XN) - (float)(mu * Ws[k]);
         if (v >= cmax - delta) {
             const int slot = atomicAdd(&ncand, 1);
@@ -368,7 +478,18 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
             const int l = k - L;
             const int m0 = l < 0 ? -l : 0, m1 = l > 0 ? n - l : n;
             double acc = 0.0;
-            for (int m = m0 + tid; m < m1; m += XT) acc += r0[m + l] * ((double)e[m] - mu);
+            for (int m = m0 + tid; m < m1; m += 8 * XT) {
+                double rv8[8], ev8[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {  // issue all 8 pairs of loads first
+                    const int mm = min(m + u * XT, m1 - 1);
+                    rv8[u] = r0[mm + l];
+                    ev8[u] = (double)e[mm];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (m + u * XT < m1) acc += rv8[u] * (ev8[u] - mu);
+            }
             acc = block_sum(acc, red);
             if (acc > bestd || (acc == bestd && k < kbest)) {
                 bestd = acc;
