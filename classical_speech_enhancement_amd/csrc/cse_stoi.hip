@@ -436,27 +436,26 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
     const int tid = threadIdx.x;
     // 16-kHz input samples of one staging chunk, loaded into registers one
     // chunk ahead (the global-load latency overlaps the previous chunk's
-    // resampling instead of stalling every chunk)
-    // Loads are unconditional (an out-of-range sample reads y[0] and is
-    // masked off at staging), so the compiler issues all of them back to back
-    // instead of waiting on each inside its branch.
+    // resampling instead of stalling every chunk).  The loads go through a raw
+    // buffer over the y samples finalize_enhanced keeps, src in [lo, hi) (src and
+    // src + lag inside [0, len)): the range check returns 0 for every other
+    // index, so the loads carry no masks and issue back to back.
     constexpr int PF = (SLOTS * SSTR + NT - 1) / NT;
     float pre[PF];
-    unsigned pmask = 0;
+    const int lo = (int)max((int64_t)0, -(int64_t)lag);
+    const int hi = (int)min(len, len - lag);
+    const __amdgpu_buffer_rsrc_t yrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(y + lo), (short)0, 4 * max(hi - lo, 0), 0x00020000);
     auto fetch = [&](const int* tb, int c0) {
-        const int ns = min(SLOTS, tb[T_D] - c0);
-        pmask = 0;
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
             const int i = tid + u * NT;
-            const int s = i < ns * SSTR ? i / SSTR : 0, uu = i - s * SSTR;
-            const int64_t q0 = ((int64_t)HOP * tb[T_P + c0 + s]) / UP;
-            const int64_t n = 8 * q0 + KLO + uu;  // e index (finalize_enhanced output)
-            const int64_t src = n - lag;         // y index
-            const bool ok = i < ns * SSTR && uu < 8 * GRP + KN && n >= 0 && n < len &&
-                            src >= 0 && src < len && !(CSE_STOI_ABLATE & 16);
-            pre[u] = y[ok ? src : 0];
-            pmask |= (ok ? 1u : 0u) << u;
+            const int s = i / SSTR, uu = i - s * SSTR;  // s may pass the chunk: staged never
+            const int q0 = (HOP * tb[T_P + c0 + s]) / UP;
+            const int src = 8 * q0 + KLO + uu - lag - lo;  // negative -> out of range -> 0
+            const float t = __builtin_bit_cast(
+                float, __builtin_amdgcn_raw_buffer_load_b32(yrc, 4 * src, 0, 0));
+            pre[u] = (uu < 8 * GRP + KN && !(CSE_STOI_ABLATE & 16)) ? t : 0.0f;
         }
     };
     if (nblk > 0) {
@@ -488,8 +487,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                     const int s = i / SSTR, uu = i - s * SSTR;
                     float v = pre[u];
                     if (clip) v = fminf(fmaxf(v, -1.0f), 1.0f);
-                    if (i < ns * SSTR)
-                        L.u.a.stage[s * SSTR + (uu & 7) * SROW + (uu >> 3)] = ((pmask >> u) & 1) ? v : 0.0f;
+                    if (i < ns * SSTR) L.u.a.stage[s * SSTR + (uu & 7) * SROW + (uu >> 3)] = v;
                 }
                 __syncthreads();  // stage (and the next block's table) visible
                 if (c0 + SLOTS < D)
@@ -717,10 +715,24 @@ __global__ void __launch_bounds__(stoi::NT, 3) stoi_cells_kernel(StoiArgs a,
     for (int j0 = 0; j0 < ((CSE_STOI_ABLATE & 8) ? 0 : J); j0 += 64) {
         const int rows = min(64, J - j0) + NSEG - 1;
         __syncthreads();
-        for (int i = tid; i < rows * 16; i += NT) {
-            const int r = i >> 4, b = i & 15;
-            L.u.b.y[r * 17 + b] = env[(int64_t)(j0 + r) * 16 + b];
-            L.u.b.x[r * 17 + b] = xt[(int64_t)(j0 + r) * 16 + b];
+        {   // the tile's <= 6 rows per lane of both envelopes: every load issued
+            // before the first store (clamped indices, masked stores)
+            constexpr int TU = (94 * 16 + NT - 1) / NT;
+            double ty[TU], tx[TU];
+#pragma unroll
+            for (int u = 0; u < TU; ++u) {
+                const int i = min(tid + u * NT, rows * 16 - 1);
+                ty[u] = env[(int64_t)j0 * 16 + i];
+                tx[u] = xt[(int64_t)j0 * 16 + i];
+            }
+#pragma unroll
+            for (int u = 0; u < TU; ++u) {
+                const int i = tid + u * NT;
+                if (i < rows * 16) {
+                    L.u.b.y[(i >> 4) * 17 + (i & 15)] = ty[u];
+                    L.u.b.x[(i >> 4) * 17 + (i & 15)] = tx[u];
+                }
+            }
         }
         __syncthreads();
         const int j = j0 + seg;

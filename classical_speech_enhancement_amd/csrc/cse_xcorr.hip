@@ -25,6 +25,8 @@
 // fp32 argmax and reports status CSE_XCORR_AMBIGUOUS.
 #include "cse_common.hpp"
 
+#include <type_traits>
+
 namespace cse {
 
 constexpr int XN = 8192;      // real transform length of one block correlation
@@ -336,22 +338,35 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     const float2* Rs = a.R + (int64_t)sig * a.nb * (XH + 1);
     const cf rot_tid = bin_rotor(tid);
     const int pt = px(tid), mb = mirror_base(tid);
-    // raw buffer over e[0, n): out-of-range loads return 0 (CDNA buffer
-    // resource, word 3 = 0x00020000: 32-bit data format, no swizzle)
+    // raw buffer over e[0, n) (CDNA buffer resource, word 3 = 0x00020000:
+    // 32-bit data format, no swizzle)
     const __amdgpu_buffer_rsrc_t erc =
         __builtin_amdgcn_make_buffer_rsrc((void*)e, (short)0, 4 * n, 0x00020000);
 #pragma unroll 1
     for (int b = 0; b < a.nb; ++b) {
         // samples v = 2 tid + (u & 1) + 512 (u >> 1) of the block; v < XB needs
-        // u >> 1 <= 9 (and tid < 192 at 9); q >= n reads 0 (buffer range check)
+        // u >> 1 <= 9 (and tid < 192 at 9).  Offsets are clamped to the last
+        // sample in the last block (q >= n is masked to 0 here): the clamp also
+        // keeps the compiler from fusing a sample pair into one 8-byte load, which
+        // the range check would zero as a whole when only its second sample is
+        // past n.  Blocks
+        // before the last lie inside [0, n) and keep the fused loads.
         float x[20];
+        auto load_block = [&](auto last) {
 #pragma unroll
-        for (int u = 0; u < 20; ++u) {
-            const int v = 2 * tid + (u & 1) + 2 * XT * (u >> 1);
-            const float t = __builtin_bit_cast(  // the builtin returns the raw 32 bits
-                float, __builtin_amdgcn_raw_buffer_load_b32(erc, 4 * (b * XB + v), 0, 0));
-            x[u] = (u < 18 || v < XB) ? t : 0.0f;
-        }
+            for (int u = 0; u < 20; ++u) {
+                const int v = 2 * tid + (u & 1) + 2 * XT * (u >> 1);
+                const int q = b * XB + v;
+                const int qc = decltype(last)::value ? min(q, n - 1) : q;
+                const float t = __builtin_bit_cast(  // the builtin returns the raw 32 bits
+                    float, __builtin_amdgcn_raw_buffer_load_b32(erc, 4 * qc, 0, 0));
+                x[u] = ((u < 18 || v < XB) && (!decltype(last)::value || q < n)) ? t : 0.0f;
+            }
+        };
+        if (b + 1 < a.nb)
+            load_block(std::false_type());
+        else
+            load_block(std::true_type());
 #pragma unroll
         for (int u = 0; u < 20; ++u) {
             s1 += (double)x[u];

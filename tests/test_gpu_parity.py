@@ -240,6 +240,32 @@ def test_alignment_lags_10s_vs_oracle(P):
         assert abs(snr_db(res["sse"][j:j + 1], ps)[0] - ref) < 2e-4, (name, p)
 
 
+@pytest.mark.parametrize("length", [4993, 7999, 9985])
+def test_alignment_odd_and_block_edge_lengths(P, length):
+    """Correlated heads of odd length and of one sample past a 4992-sample
+    block boundary (4993, 9985): the last block's final sample must be read,
+    the samples past n must not (lags and aligned SNR vs the oracle)."""
+    import torch
+    from classical_speech_enhancement_amd.engine import Engine, snr_db
+    clean, noisy = make_pair(11, seconds=0.7)
+    clean, noisy = clean[:length].copy(), noisy[:length].copy()
+    eng = Engine()
+    x = torch.as_tensor(noisy).cuda().view(1, -1)
+    c = torch.as_tensor(clean).cuda().view(1, -1)
+    rng = np.random.default_rng(length)
+    grid = [p for p in oracle.grid_cells(oracle.GRIDS["mmse"]) if p["n_fft"] == 512]
+    cells = [grid[i] for i in rng.choice(len(grid), 8, replace=False)]
+    res = eng.run(x, [(0, "mmse", p) for p in cells], clean=c, align=True)
+    assert (res["xcorr_status"] == 0).all()
+    ps = float(np.sum(clean ** 2))
+    for j, p in enumerate(cells):
+        y = oracle.ALGORITHMS["mmse"](noisy, 16000, **p)
+        lag = oracle.align_lag(clean, y, 16000)
+        assert res["lag"][j] == (lag or 0), (p, res["lag"][j], lag)
+        ref = oracle.calculate_snr(clean, oracle.finalize_enhanced(y, clean, 16000))
+        assert abs(snr_db(res["sse"][j:j + 1], ps)[0] - ref) < 2e-4, p
+
+
 @pytest.mark.parametrize("n_fft", [512, 1024])
 @pytest.mark.parametrize("alg", ["spectralSubtractor", "wiener", "mmse", "omlsa"])
 def test_full_size_grid_properties(alg, n_fft):
