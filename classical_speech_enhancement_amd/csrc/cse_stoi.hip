@@ -45,13 +45,6 @@
 
 namespace cse {
 
-// CSE_STOI_ABLATE (timing experiments only; 0 in product builds): skip
-//   1 = resampling arithmetic, 2 = FFT, 4 = band sums, 8 = phase B,
-//   16 = input loads (staged zeros), 32 = overlap-add
-#ifndef CSE_STOI_ABLATE
-#define CSE_STOI_ABLATE 0
-#endif
-
 namespace stoi {
 constexpr int UP = 5, DOWN = 8;          // 10 kHz / 16 kHz
 constexpr int HALF_LEN = 290;            // (581 - 1) / 2
@@ -455,7 +448,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
             const int src = 8 * q0 + KLO + uu - lag - lo;  // negative -> out of range -> 0
             const float t = __builtin_bit_cast(
                 float, __builtin_amdgcn_raw_buffer_load_b32(yrc, 4 * src, 0, 0));
-            pre[u] = (uu < 8 * GRP + KN && !(CSE_STOI_ABLATE & 16)) ? t : 0.0f;
+            pre[u] = (uu < 8 * GRP + KN) ? t : 0.0f;
         }
     };
     if (nblk > 0) {
@@ -494,7 +487,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                     fetch(tb, c0 + SLOTS);
                 else if (blk + 1 < nblk)
                     fetch(tn, 0);
-                if (tid < ns * GRP && !(CSE_STOI_ABLATE & 1)) {
+                if (tid < ns * GRP) {
                     const int s = tid / GRP, g = tid - s * GRP;
                     const int64_t p = tb[T_P + c0 + s];
                     const int64_t q0 = (HOP * p) / UP;
@@ -539,7 +532,6 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
             }
         }
         __syncthreads();
-        if (!(CSE_STOI_ABLATE & 2))
         // ---- 512-point rfft of frame fl, 16 lanes per frame: sample n of the
         // frame is w[n] ola[fl + n/128][n mod 128], the overlap-added row
         // ola[hl][o] = w[o] e10[sa][o] + w[128 + o] e10[sb][o] read straight
@@ -610,7 +602,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
         }
         __syncthreads();
         // ---- band envelopes
-        if (tid < nf * NBAND && !(CSE_STOI_ABLATE & 4)) {
+        if (tid < nf * NBAND) {
             const int fl = tid / NBAND, b = tid - fl * NBAND;
             const double* pw = L.u.t[fl];
             double s = 0.0;
@@ -712,7 +704,7 @@ __global__ void __launch_bounds__(stoi::NT, 3) stoi_cells_kernel(StoiArgs a,
     constexpr double clipf = 6.623413251903491;  // 1 + 10^(-BETA/20)
     double dsum = 0.0;
     const int seg = tid & 63, bg = tid >> 6;
-    for (int j0 = 0; j0 < ((CSE_STOI_ABLATE & 8) ? 0 : J); j0 += 64) {
+    for (int j0 = 0; j0 < J; j0 += 64) {
         const int rows = min(64, J - j0) + NSEG - 1;
         __syncthreads();
         {   // the tile's <= 6 rows per lane of both envelopes: every load issued
