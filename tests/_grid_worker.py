@@ -73,7 +73,7 @@ def rank_main(rank, world, port, outdir):
         table, best = search.run_grid(clean, noisy, specs, compute=compute)
         win = np.array([[k[0], list(SMALL_GRIDS).index(k[1]), v[0]] for k, v in best.items()])
         np.savez(os.path.join(outdir, f"rank{rank}.npz"), table=table, win=win,
-                 ids=np.array(calls[0] if calls else [], dtype=np.int64))
+                 ids=np.array([i for c in calls for i in c], dtype=np.int64))
     finally:
         dist.destroy_process_group()
 

@@ -1,5 +1,5 @@
 """Grid-search driver: enumeration order, LPT sharding, the records gather
-over world_size 2 (gloo, CPU) and the reference's sequential selection
+over world_size 2 and 4 (gloo, CPU) and the reference's sequential selection
 (speech_enhancement_comparison.py:149-216)."""
 
 import socket
@@ -86,22 +86,24 @@ def _free_port():
     return port
 
 
-def test_run_grid_world2_gloo_matches_single_process(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_run_grid_gloo_matches_single_process(tmp_path, world):
+    """world 2 and 4 (rehearsing the 8-GPU node's sharding on CPU ranks)."""
     import torch.multiprocessing as tmp
-    tmp.spawn(rank_main, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    r0 = np.load(tmp_path / "rank0.npz")
-    r1 = np.load(tmp_path / "rank1.npz")
+    tmp.spawn(rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    rs = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     clean, noisy = pairs()
     specs = search.job_specs(len(noisy), grids=SMALL_GRIDS)
     ref = oracle_compute(clean, noisy, specs, np.arange(len(specs)))
     # every rank holds the full table, identical to one process computing all cells
-    assert np.array_equal(r0["table"], ref) and np.array_equal(r1["table"], ref)
-    assert np.array_equal(r0["win"], r1["win"])
-    # the two shards are disjoint and cover the job
-    ids = np.concatenate([r0["ids"], r1["ids"]])
+    for r in rs:
+        assert np.array_equal(r["table"], ref)
+        assert np.array_equal(r["win"], rs[0]["win"])
+    # the shards are disjoint and cover the job
+    ids = np.concatenate([r["ids"] for r in rs])
     assert sorted(ids.tolist()) == list(range(len(specs)))
     best = search.select_best(specs, ref)
-    assert [v[0] for v in best.values()] == r0["win"][:, 2].tolist()
+    assert [v[0] for v in best.values()] == rs[0]["win"][:, 2].tolist()
 
 
 def test_optimize_parameters_mirror():
