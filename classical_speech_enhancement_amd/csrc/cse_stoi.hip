@@ -528,10 +528,10 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                         if (off >= 0 && off < HOP) L.u.a.e10[c0 + s][off] = acc[r];
                     }
                 }
-                __syncthreads();
+                __syncthreads();  // e10 complete (also ends the chunk loop's last pass)
             }
         }
-        __syncthreads();
+        if (PRE) __syncthreads();
         // ---- 512-point rfft of frame fl, 16 lanes per frame: sample n of the
         // frame is w[n] ola[fl + n/128][n mod 128], the overlap-added row
         // ola[hl][o] = w[o] e10[sa][o] + w[128 + o] e10[sb][o] read straight
@@ -599,15 +599,14 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                 const cd x = dadd(e, dmul(L.tw512[k], od));  // X[k] = E + e^{-2πi k/512} O
                 if (k < 224) pw[k] = fma(x.x, x.x, x.y * x.y);
             }
-        }
-        __syncthreads();
-        // ---- band envelopes
-        if (tid < nf * NBAND) {
-            const int fl = tid / NBAND, b = tid - fl * NBAND;
-            const double* pw = L.u.t[fl];
-            double s = 0.0;
-            for (int k = BAND_EDGE[b]; k < BAND_EDGE[b + 1]; ++k) s += pw[k];
-            env[(int64_t)(j0 + fl) * 16 + b] = sqrt(s);
+            // ---- band envelopes of the frame by its own 16 lanes (one wave:
+            // no workgroup barrier; the next block's first barrier protects pw)
+            wave_sync();
+            if (n1 < NBAND && fl < nf) {
+                double s = 0.0;
+                for (int k = BAND_EDGE[n1]; k < BAND_EDGE[n1 + 1]; ++k) s += pw[k];
+                env[(int64_t)(j0 + fl) * 16 + n1] = sqrt(s);
+            }
         }
     }
 }
