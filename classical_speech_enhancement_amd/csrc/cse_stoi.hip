@@ -433,23 +433,32 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
     // buffer over the y samples finalize_enhanced keeps, src in [lo, hi) (src and
     // src + lag inside [0, len)): the range check returns 0 for every other
     // index, so the loads carry no masks and issue back to back.
-    constexpr int PF = (SLOTS * SSTR + NT - 1) / NT;
+    // Lane tid stages slot fs = tid / FW (FW = 28 lanes per slot, 9 slots), samples
+    // uu = fr + FW u: one block-table read and one base index per fetch, the
+    // loads at constant strides from it
+    constexpr int FW = 28, NU = 8 * GRP + KN;             // NU = 339 samples staged per slot
+    constexpr int PF = (NU + FW - 1) / FW;                // 13 loads per lane
+    static_assert(SLOTS * FW <= NT, "staging lanes");
+    const int fs = tid / FW, fr = tid - FW * (tid / FW);
+    // finalize_enhanced keeps y[src] for src and src + lag inside [0, len):
+    // src - lo in [0, cnt).  Indices are clamped into that range for the load and
+    // the sample is zeroed at staging when it was outside (no reliance on the
+    // buffer range check, which does not see a folded immediate offset).
     float pre[PF];
     const int lo = (int)max((int64_t)0, -(int64_t)lag);
-    const int hi = (int)min(len, len - lag);
+    const int cnt = max((int)min(len, len - lag) - lo, 0);
     const __amdgpu_buffer_rsrc_t yrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(y + lo), (short)0, 4 * max(hi - lo, 0), 0x00020000);
+        (void*)(y + lo), (short)0, 4 * cnt, 0x00020000);
+    int fbase = 0;  // src - lo of the lane's sample uu = fr in the fetched chunk
     auto fetch = [&](const int* tb, int c0) {
+        // lanes past the 9 slots (and slots past the chunk) read a table entry
+        // in range and are never staged
+        const int q0 = (HOP * tb[T_P + c0 + min(fs, SLOTS - 1)]) / UP;
+        fbase = 8 * q0 + KLO + fr - lag - lo;
 #pragma unroll
-        for (int u = 0; u < PF; ++u) {
-            const int i = tid + u * NT;
-            const int s = i / SSTR, uu = i - s * SSTR;  // s may pass the chunk: staged never
-            const int q0 = (HOP * tb[T_P + c0 + s]) / UP;
-            const int src = 8 * q0 + KLO + uu - lag - lo;  // negative -> out of range -> 0
-            const float t = __builtin_bit_cast(
-                float, __builtin_amdgcn_raw_buffer_load_b32(yrc, 4 * src, 0, 0));
-            pre[u] = (uu < 8 * GRP + KN) ? t : 0.0f;
-        }
+        for (int u = 0; u < PF; ++u)
+            pre[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                yrc, 4 * min(max(fbase + FW * u, 0), max(cnt - 1, 0)), 0, 0));
     };
     if (nblk > 0) {
         __syncthreads();
@@ -473,14 +482,16 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
         } else {
             for (int c0 = 0; c0 < D; c0 += SLOTS) {
                 const int ns = min(SLOTS, D - c0);
-                // stage e[8 q0 - 58 + u], u < 339, at [u & 7][u >> 3]
+                // stage e[8 q0 - 58 + uu], uu < 339, at [uu & 7][uu >> 3]
+                if (fs < ns) {
+                    float* st = L.u.a.stage + fs * SSTR;
 #pragma unroll
-                for (int u = 0; u < PF; ++u) {
-                    const int i = tid + u * NT;
-                    const int s = i / SSTR, uu = i - s * SSTR;
-                    float v = pre[u];
-                    if (clip) v = fminf(fmaxf(v, -1.0f), 1.0f);
-                    if (i < ns * SSTR) L.u.a.stage[s * SSTR + (uu & 7) * SROW + (uu >> 3)] = v;
+                    for (int u = 0; u < PF; ++u) {
+                        const int uu = fr + FW * u;
+                        float v = (unsigned)(fbase + FW * u) < (unsigned)cnt ? pre[u] : 0.0f;
+                        if (clip) v = fminf(fmaxf(v, -1.0f), 1.0f);
+                        if (u < PF - 1 || uu < NU) st[(uu & 7) * SROW + (uu >> 3)] = v;
+                    }
                 }
                 __syncthreads();  // stage (and the next block's table) visible
                 if (c0 + SLOTS < D)
