@@ -28,7 +28,7 @@ PATCHES = [
         "        if (false)\n        // ---- 512-point rfft of frame fl, 16 lanes per frame"),
     (4, "if (tid < nf * NBAND) {", "if (false) {"),
     (8, "for (int j0 = 0; j0 < J; j0 += 64) {", "for (int j0 = 0; j0 < 0; j0 += 64) {"),
-    (16, "pre[u] = (uu < 8 * GRP + KN) ? t : 0.0f;", "pre[u] = 0.0f;"),
+    (16, "float v = (unsigned)(fbase + FW * u) < (unsigned)cnt ? pre[u] : 0.0f;", "float v = 0.0f;"),
 ]
 
 
