@@ -339,18 +339,18 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     const cf rot_tid = bin_rotor(tid);
     const int pt = px(tid), mb = mirror_base(tid);
     // raw buffer over e[0, n) (CDNA buffer resource, word 3 = 0x00020000:
-    // 32-bit data format, no swizzle)
+    // 32-bit data format, no swizzle); every offset issued lies inside it
     const __amdgpu_buffer_rsrc_t erc =
         __builtin_amdgcn_make_buffer_rsrc((void*)e, (short)0, 4 * n, 0x00020000);
 #pragma unroll 1
     for (int b = 0; b < a.nb; ++b) {
         // samples v = 2 tid + (u & 1) + 512 (u >> 1) of the block; v < XB needs
-        // u >> 1 <= 9 (and tid < 192 at 9).  Offsets are clamped to the last
-        // sample in the last block (q >= n is masked to 0 here): the clamp also
-        // keeps the compiler from fusing a sample pair into one 8-byte load, which
-        // the range check would zero as a whole when only its second sample is
-        // past n.  Blocks
-        // before the last lie inside [0, n) and keep the fused loads.
+        // u >> 1 <= 9 (and tid < 192 at 9).  In the last block the offsets are
+        // clamped to the last sample and q >= n is masked to 0 here: the buffer
+        // range check is not relied on (it misses a constant part the compiler
+        // folds into the instruction's immediate offset, and a fused 8-byte
+        // sample pair can straddle n).  Blocks before the last lie inside
+        // [0, n) and keep the fused loads.
         float x[20];
         auto load_block = [&](auto last) {
 #pragma unroll
