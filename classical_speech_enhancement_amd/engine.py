@@ -14,6 +14,7 @@ the reference plugin's keyword arguments (parameter_ranges.py keys).
 
 import ctypes
 import math
+from collections import OrderedDict
 
 import numpy as np
 import torch
@@ -136,7 +137,10 @@ class Engine:
         if not torch.cuda.is_available():
             raise _lib.CseError("no GPU visible: the HIP engine has no CPU fallback")
         self.device = torch.device(device)
-        self._plan_cache = None  # (key, specs, MultiPlan): see run(reuse=True)
+        # key -> ((specs, keep), MultiPlan), most recent last: see run(reuse=...)
+        self._plan_cache = OrderedDict()
+        self.plan_cache_size = 1
+        self._side = None
 
     # ------------------------------------------------------------------ prep
     def stft(self, x, n_fft, hop, x_sub=None, want_y=True, want_p=True):
@@ -196,8 +200,15 @@ class Engine:
         return MultiPlan(self, n_signals, length, specs, with_clean, want_waveforms, want_gains,
                          align, true_len)
 
+    def side_stream(self):
+        """A second stream of this engine, kept for its lifetime (work queued
+        on it reuses the caching allocator's blocks of earlier calls)."""
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
     def run(self, noisy, specs, clean=None, want_waveforms=False, want_gains=False, align=False,
-            true_len=None, reuse=None, keep=None):
+            true_len=None, reuse=None, keep=None, on_plan=None):
         """Enhance every cell spec; returns a dict of per-spec results.
 
         noisy/clean: [S, L] float64 cuda tensors (clean may be None if no spec
@@ -208,8 +219,8 @@ class Engine:
         true_len: TrueNoise estimates use the first true_len samples of noisy
         and clean (a clean reference shorter than the noisy signal,
         noise_estimation.py:128-130); default L.
-        reuse: keep the plan (device buffers, cell tables) for the next call
-        with the same structure.  True: the structure is spec_fingerprint(specs)
+        reuse: keep the plan (device buffers, cell tables) for a later call
+        with the same structure (the plan_cache_size most recent ones).  True: the structure is spec_fingerprint(specs)
         — per cell the signal index, algorithm and params object identity (the
         cached specs keep the params alive; they must not be mutated in
         between).  Or a hashable key the caller derived from the structure;
@@ -217,6 +228,7 @@ class Engine:
         only when the key misses, and ``keep`` is held with the plan (the
         object the key's identities refer to).  The results' 'y' is the plan's
         buffer: the next reusing call overwrites it.
+        on_plan: see MultiPlan.execute.
         """
         S, L = noisy.shape
         flags = (S, L, clean is not None, want_waveforms, want_gains, align, true_len)
@@ -226,15 +238,20 @@ class Engine:
                 specs = specs() if callable(specs) else specs
                 reuse = spec_fingerprint(specs)
             key = flags + (reuse,)
-            c = self._plan_cache
-            if c is not None and c[0] == key:
-                mp = c[2]
+            hit = self._plan_cache.get(key)
+            if hit is not None:
+                mp = hit[1]
+                self._plan_cache.move_to_end(key)
         if mp is None:
             specs = specs() if callable(specs) else specs
+            if key is not None:  # evict before allocating the new plan's buffers
+                while len(self._plan_cache) >= max(self.plan_cache_size, 1):
+                    self._plan_cache.popitem(last=False)
             mp = self.plan(S, L, specs, clean is not None, want_waveforms, want_gains, align,
                            true_len)
-            self._plan_cache = (key, (specs, keep), mp) if key is not None else None
-        mp.execute(noisy, clean)
+            if key is not None:
+                self._plan_cache[key] = ((specs, keep), mp)
+        mp.execute(noisy, clean, on_plan)
         return mp.results()
 
 
@@ -546,9 +563,24 @@ class MultiPlan:
                       for n_fft, items in sorted(by_fft.items())]
         self.units = sum(p.units for p in self.plans)
 
-    def execute(self, noisy, clean=None):
-        for p in self.plans:
-            p.execute(noisy, clean)
+    def execute(self, noisy, clean=None, on_plan=None):
+        """Per n_fft: analysis (STFTs, noise rows), enhance, alignment.
+        on_plan(plan, sse, finite, lag): called once an n_fft's cells are final
+        (host-synchronised results in plan.items order; plan.idx maps them to
+        spec indices), after the next n_fft's analysis is queued and before its
+        enhance is, so the caller can queue work on those cells' outputs on
+        another stream without starving the next analysis' small kernels."""
+        if self.plans:
+            self.plans[0].prepare(noisy, clean)
+        for k, p in enumerate(self.plans):
+            p.enhance()
+            if p.align:
+                p.finalize()
+            if k + 1 < len(self.plans):
+                self.plans[k + 1].prepare(noisy, clean)
+            if on_plan is not None:
+                sse, fin, _ = p.results()
+                on_plan(p, sse, fin, p.lag)
 
     def results(self):
         sse = np.full(self.n, np.nan)

@@ -74,19 +74,30 @@ class StoiPlan:
         y: flat f32 cuda tensor holding every cell's output (>= L samples from
         y_offset[c]); sig_of: clean signal of each cell; lag: alignment lag
         (None = 0).  The test signal of cell c is y[n - lag] (zero outside
-        [0, L)), clipped to [-1, 1] when clip."""
+        [0, L)), clipped to [-1, 1] when clip.  y_offset / sig_of / lag given
+        as host arrays are validated here and uploaded on the current stream;
+        given as cuda tensors (int64 / int32 / int32) they are taken as they
+        are, with no host synchronisation (the caller validated them)."""
         dev = self.clean.device
-        off = torch.as_tensor(np.asarray(y_offset, dtype=np.int64), device=dev)
-        sig = torch.as_tensor(np.asarray(sig_of, dtype=np.int32), device=dev)
-        n = int(off.numel())
-        if sig.numel() != n:
-            raise ValueError("y_offset and sig_of differ in length")
-        if n and (int(sig.min()) < 0 or int(sig.max()) >= self.S):
-            raise ValueError("sig_of out of range")
-        if n and (int(off.min()) < 0 or int(off.max()) + self.L > y.numel()):
-            raise ValueError("a cell's output runs past the end of y")
         if y.dtype != torch.float32 or not y.is_cuda:
             raise ValueError("y must be a float32 cuda tensor")
+        if torch.is_tensor(y_offset):
+            off, sig = y_offset, sig_of
+            n = int(off.numel())
+            if int(sig.numel()) != n:
+                raise ValueError("y_offset and sig_of differ in length")
+        else:
+            off_h = np.asarray(y_offset, dtype=np.int64)
+            sig_h = np.asarray(sig_of, dtype=np.int32)
+            n = len(off_h)
+            if len(sig_h) != n:
+                raise ValueError("y_offset and sig_of differ in length")
+            if n and (int(sig_h.min()) < 0 or int(sig_h.max()) >= self.S):
+                raise ValueError("sig_of out of range")
+            if n and (int(off_h.min()) < 0 or int(off_h.max()) + self.L > y.numel()):
+                raise ValueError("a cell's output runs past the end of y")
+            off = torch.as_tensor(off_h, device=dev)
+            sig = torch.as_tensor(sig_h, device=dev)
         lg = None
         if lag is not None:
             lg = torch.as_tensor(np.asarray(lag, dtype=np.int32), device=dev) \
