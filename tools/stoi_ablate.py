@@ -8,6 +8,7 @@ stage of stoi_cells_kernel switched off, and builds a libcse variant from it
       1  resampling arithmetic          2  rfft of the frames
       4  band sums                      8  phase B (segment correlations)
       16 16-kHz input loads (zeros staged)
+      64 occupancy probe: 2 instead of 3 workgroups per CU (extra unused LDS)
 
 The outputs of such a build are wrong by construction (tools/ab_stoi.sh runs
 tools/bench_stoi.py with CSE_BENCH_NOCHECK=1).  DESIGN.md §3.5 records the
@@ -29,6 +30,9 @@ PATCHES = [
     (4, "if (tid < nf * NBAND) {", "if (false) {"),
     (8, "for (int j0 = 0; j0 < J; j0 += 64) {", "for (int j0 = 0; j0 < 0; j0 += 64) {"),
     (16, "float v = (unsigned)(fbase + FW * u) < (unsigned)cnt ? pre[u] : 0.0f;", "float v = 0.0f;"),
+    # occupancy probe (not a stage): 14 KiB of unused dynamic LDS per workgroup,
+    # 3 -> 2 workgroups per CU
+    (64, "dim3((unsigned)n_cells), dim3(stoi::NT), 0,", "dim3((unsigned)n_cells), dim3(stoi::NT), 14336,"),
 ]
 
 
