@@ -217,7 +217,7 @@ def test_grid_snr_aligned_matches_reference(P):
 def test_alignment_lags_10s_vs_oracle(P):
     """10-s pair: device lags and aligned SNR of sampled MMSE / SS cells against
     the oracle's align_lag / finalize on its own fp64 outputs (n = 32000
-    correlated samples, 8 FFT blocks)."""
+    correlated samples, 7 FFT blocks of 4,992)."""
     import torch
     from classical_speech_enhancement_amd.engine import Engine, snr_db
     clean, noisy = make_pair(5, seconds=10.0)
