@@ -44,7 +44,7 @@ sys.path.insert(0, REPO)
 METRIC = ("STFT frame-gain evals/sec/node, 16kHz 512-pt FFT full grid; 1/2/4/8-GPU scaling")
 HBM_PEAK = 8.0e12              # MI355X_MICROARCH.md: 8.0 TB/s spec
 SIMDS = 1024                   # 256 CUs x 4 SIMD-32
-VALU_CYC, TRANS_CYC = 2, 8     # wave64 issue cycles: v_fma_f32 (SIMD-32), transcendental (1/4 rate)
+VALU_CYC, TRANS_CYC = 2, 4     # wave64 issue cycles: v_fma_f32 (SIMD-32), transcendental (2x: tools/micro/valu_rate.hip)
 CLOCK = 2.4e9                  # max shader clock
 TOL = 1e-5                     # north-star relative waveform tolerance
 SNR_TOL_DB = 2e-4              # per-cell SNR tolerance of the parity tests

@@ -5,7 +5,7 @@ and calls, and the PMC counters of the separate --pmc passes, per launch
 (counter sum over the profiled launches / launches).  HBM traffic per launch =
 (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 (gfx950 correction, MI355X_MICROARCH.md
 HBM/rocprofv3 section: FETCH_SIZE counts half the bytes of wide streaming reads).
-VALU issue fraction = (2 x (VALU - TRANS) + 8 x TRANS) SIMD cycles (fp64 FMA/MUL/ADD
+VALU issue fraction = (2 x (VALU - TRANS) + 4 x TRANS) SIMD cycles (fp64 FMA/MUL/ADD
 at 4) over 1024 SIMDs x SQ_BUSY_CYCLES / 32 (per-shader-engine cycles with
 waves resident, summed over the 32 SEs).  GRBM_GUI_ACTIVE / 8 read twice the
 shader clock on the r02 boxes, so it is only recorded.
@@ -25,7 +25,7 @@ import sys
 REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 KERNELS = {"enhance512": "enhance_kernel<512, false>", "enhance1024": "enhance_kernel<1024, false>",
            "stoi": "stoi_cells_kernel", "xcorr_lag": "xcorr_lag_kernel"}
-SIMDS, VALU_CYC, TRANS_CYC = 1024, 2, 8
+SIMDS, VALU_CYC, TRANS_CYC = 1024, 2, 4  # transcendental = 2x v_fma_f32 (tools/micro/valu_rate.hip)
 
 
 def stats(path):
