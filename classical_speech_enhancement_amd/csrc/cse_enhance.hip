@@ -234,14 +234,6 @@ static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
 #define CSE_WAVES_PER_SIMD 3
 #endif
 
-// hide a value's provenance from the optimiser (keeps derived per-lane
-// addresses/rotors from being hoisted into long-lived registers)
-template <typename T>
-__device__ __forceinline__ T opaque(T x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-
 // Ordering of LDS accesses between the lanes of ONE wave: the LDS executes a
 // wave's DS instructions in issue order, so a compiler-level barrier is all a
 // write->read or read->write hand-off inside the wave needs (no s_waitcnt).
@@ -532,20 +524,20 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             __builtin_amdgcn_s_setprio(1);
             cf z[16];
             {
-                const CellParam cpar = *(const CellParam*)(smem + opaque(W::OFF_CP + 32 * cslot));
+                const CellParam cpar = *(const CellParam*)(smem + W::OFF_CP + 32 * cslot);
                 const float alpha_t = (t == 0) ? 0.0f : cpar.p0;  // see gain_wiener
-                const cf base = *(const cf*)(smem + opaque(W::OFF_LC + 8 * i));
+                const cf base = *(const cf*)(smem + W::OFF_LC + 8 * i);
                 const int yb = W::OFF_Y + (t & 1) * W::YROW, gb = W::OFF_G + (t & 1) * W::GROW;
                 // mirror halves: lane i's slot e (9 entries, 72 B) receives
                 // Z'[M - i - L e] (e < 8) and Z'[M/2] (e = 8); lane q takes
                 // z[s] (s >= 8) = Z'[q + L s] from lane (L - q) mod L, entry 15 - s
                 // (lane 0: its own entry 16 - s, entry 8 = Z'[M/2] for s = 8)
                 gain_pack<NFFT, ALGO, OUT>(
-                    (const float2*)(smem + opaque(yb + 8 * i)), (const float*)(smem + opaque(gb + 4 * i)),
-                    (const float2*)(smem + opaque(yb + 8 * (M - i - 7 * L))),
-                    (const float*)(smem + opaque(gb + 4 * (M - i - 7 * L))),
+                    (const float2*)(smem + yb + 8 * i), (const float*)(smem + gb + 4 * i),
+                    (const float2*)(smem + yb + 8 * (M - i - 7 * L)),
+                    (const float*)(smem + gb + 4 * (M - i - 7 * L)),
                     (const float2*)(smem + yb + 8 * MH), (const float*)(smem + gb + 4 * MH), z,
-                    (cf*)(smem + opaque(creg + 72 * i)), rr, alpha_t, cpar, base,
+                    (cf*)(smem + creg + 72 * i), rr, alpha_t, cpar, base,
                     (OUT && gout) ? gout + t * B : nullptr, i);
             }
             __builtin_amdgcn_s_setprio(0);
@@ -553,7 +545,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             wave_sync();  // my wave's mirror entries written
             {
                 const int partner = (L - i) & (L - 1);
-                const cf* xr = (const cf*)(smem + opaque(creg + 72 * partner + (i == 0 ? 8 : 0)));
+                const cf* xr = (const cf*)(smem + creg + 72 * partner + (i == 0 ? 8 : 0));
 #pragma unroll
                 for (int s = 8; s < 16; ++s) z[s] = xr[15 - s];
             }
@@ -565,7 +557,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             {
                 // pass-1 twiddles e^{2πi i' b/M}, b = 1..15, of my column (per-lane
                 // row of 18 complex: 8 ds_read_b128), issued ahead of the DFT
-                const float4* twr = (const float4*)(smem + opaque(W::OFF_TW + 144 * ((L == 16) ? i : b2)));
+                const float4* twr = (const float4*)(smem + W::OFF_TW + 144 * ((L == 16) ? i : b2));
                 float4 t4[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) t4[k] = twr[k];
@@ -592,8 +584,8 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             {
                 constexpr int TS = W::TS;
                 wave_sync();  // my wave's mirror reads are issued before the transpose overwrites
-                cf* tw_ = (cf*)(smem + opaque(creg + 8 * i));              // + 8 TS b
-                const cf* tr = (const cf*)(smem + opaque(creg + 8 * TS * b2));  // + 8 r
+                cf* tw_ = (cf*)(smem + creg + 8 * i);              // + 8 TS b
+                const cf* tr = (const cf*)(smem + creg + 8 * TS * b2);  // + 8 r
 #pragma unroll
                 for (int b = 0; b < 16; ++b) tw_[b * TS] = z[b];
                 wave_sync();
@@ -638,7 +630,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         // the lane's window slots: ds_read_b128 from its 16-B aligned table row
         float wv[W::WSLOTS];
         {
-            const float4* w4 = (const float4*)(smem + opaque(W::OFF_WIN + 4 * W::WSTR * i));
+            const float4* w4 = (const float4*)(smem + W::OFF_WIN + 4 * W::WSTR * i);
 #pragma unroll
             for (int k = 0; k < W::WSLOTS / 4; ++k) {
                 const float4 q4 = w4[k];
@@ -659,7 +651,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         if (valid) {
             const int o0 = t * HOP + off - NFFT / 2;  // output index of q = 0
             const float* crow_t = (const float*)__builtin_assume_aligned(
-                smem + opaque(W::OFF_C + (t & 1) * W::HMAX * 4 + 4 * off), 8);
+                smem + W::OFF_C + (t & 1) * W::HMAX * 4 + 4 * off, 8);
             // frame t retires output positions [t*HOP - NFFT/2, (t+1)*HOP - NFFT/2)
             // interior: every slot o and its scored clean index o + lag lie in [0, len)
             const bool edge = (t < R - 1) || (t >= nf);
@@ -669,7 +661,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             const bool head = want_y && lo < out_len;                      // uniform
             float inv[F];
             if (R == 2) {
-                const float4* it = (const float4*)(smem + opaque(W::OFF_IWS + 4 * W::ISTR * i));
+                const float4* it = (const float4*)(smem + W::OFF_IWS + 4 * W::ISTR * i);
 #pragma unroll
                 for (int k = 0; k < F / 4; ++k) {
                     const float4 q4 = it[k];
