@@ -767,8 +767,28 @@ __global__ void __launch_bounds__(WG<NFFT>::THREADS, CSE_WAVES_PER_SIMD) enhance
         dispatch_algo<NFFT, 256, OUT>(a, wcell, n, algo, smem);
 }
 
+// The two n_fft halves can be compiled as separate translation units (with
+// their own code-generation flags): cse_enhance_512.hip defines
+// CSE_ENHANCE_ONLY=512 and holds the 512 kernels, cse_enhance_1024.hip the
+// 1024 kernels and the C entry points.  Compiled on its own (analysis tools),
+// this file holds everything.
+#if !defined(CSE_ENHANCE_ONLY) || CSE_ENHANCE_ONLY == 512
+const void* enhance_fn_512(bool out) {
+    return out ? (const void*)enhance_kernel<512, true> : (const void*)enhance_kernel<512, false>;
+}
+#endif
+#if !defined(CSE_ENHANCE_ONLY) || CSE_ENHANCE_ONLY == 1024
+const void* enhance_fn_1024(bool out) {
+    return out ? (const void*)enhance_kernel<1024, true> : (const void*)enhance_kernel<1024, false>;
+}
+#endif
+#if defined(CSE_ENHANCE_ONLY) && CSE_ENHANCE_ONLY == 1024
+const void* enhance_fn_512(bool out);  // cse_enhance_512.hip
+#endif
+
 }  // namespace cse
 
+#if !defined(CSE_ENHANCE_ONLY) || CSE_ENHANCE_ONLY == 1024
 using namespace cse;
 
 extern "C" int cse_cells_per_group(int n_fft) {
@@ -805,11 +825,11 @@ extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells
     const void* fn;
     int bytes, threads;
     if (n_fft == 512) {
-        fn = out ? (const void*)enhance_kernel<512, true> : (const void*)enhance_kernel<512, false>;
+        fn = enhance_fn_512(out);
         bytes = WG<512>::BYTES;
         threads = WG<512>::THREADS;
     } else {
-        fn = out ? (const void*)enhance_kernel<1024, true> : (const void*)enhance_kernel<1024, false>;
+        fn = enhance_fn_1024(out);
         bytes = WG<1024>::BYTES;
         threads = WG<1024>::THREADS;
     }
@@ -826,3 +846,4 @@ extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells
     CSE_CHECK_LAUNCH("cse_enhance_cells");
     return CSE_OK;
 }
+#endif  // the C entry points
