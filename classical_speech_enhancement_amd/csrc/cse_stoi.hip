@@ -520,15 +520,34 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                                     acc[r] = fma(coef[r * CST + kk], e, acc[r]);
                         }
                     };
+                    // interior blocks: the 8 samples of block kb + 1 are read
+                    // from LDS while block kb's 40 FMAs run.  The coefficients
+                    // come through the scalar cache, and an s_load makes the
+                    // wait before their first use an lgkmcnt(0), which also
+                    // covers every LDS read then in flight: the next block's
+                    // reads are issued only after that wait (after tap j = 0),
+                    // so one block costs one scalar-load latency instead of a
+                    // scalar load plus four LDS round trips
+                    float sv[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) sv[j] = st[j * SROW + 1];
                     taps(std::integral_constant<int, 0>());
 #pragma unroll 1
                     for (int kb = 1; kb < 14; ++kb) {  // every tap nonzero
+                        double e[8];
 #pragma unroll
-                        for (int j = 0; j < 8; ++j) {
-                            const double e = (double)st[j * SROW + kb];
+                        for (int j = 0; j < 8; ++j) e[j] = (double)sv[j];
+#pragma unroll
+                        for (int r = 0; r < 5; ++r) acc[r] = fma(coef[r * CST + 8 * kb], e[0], acc[r]);
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) sv[j] = st[j * SROW + kb + 1];
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int j = 1; j < 8; ++j) {
 #pragma unroll
                             for (int r = 0; r < 5; ++r)
-                                acc[r] = fma(coef[r * CST + 8 * kb + j], e, acc[r]);
+                                acc[r] = fma(coef[r * CST + 8 * kb + j], e[j], acc[r]);
                         }
                     }
                     taps(std::integral_constant<int, 14>());

@@ -27,7 +27,7 @@ PATCHES = [
     (1, "if (tid < ns * GRP) {", "if (false) {"),
     (2, "        // ---- 512-point rfft of frame fl, 16 lanes per frame",
         "        if (false)\n        // ---- 512-point rfft of frame fl, 16 lanes per frame"),
-    (4, "if (tid < nf * NBAND) {", "if (false) {"),
+    (4, "if (n1 < NBAND && fl < nf) {", "if (false) {"),
     (8, "for (int j0 = 0; j0 < J; j0 += 64) {", "for (int j0 = 0; j0 < 0; j0 += 64) {"),
     (16, "float v = (unsigned)(fbase + FW * u) < (unsigned)cnt ? pre[u] : 0.0f;", "float v = 0.0f;"),
     # occupancy probe (not a stage): 14 KiB of unused dynamic LDS per workgroup,
