@@ -594,10 +594,14 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     // the read side, lane (b2, h2) takes lo = V[b2][i'], hi =
                     // V[b2][i' + 16]: U_h2[i'] = (lo + (-1)^h2 hi) W32^{i' h2},
                     // then a DFT16 over i'
+                    // branch-free on the lane's half: u = lo -/+ hi by a signed
+                    // FMA (exact), rotor (1, 0) on h2 = 0 lanes (an exact
+                    // product), so no per-element selects of whole complexes
+                    const float sg = h2 ? -1.0f : 1.0f;
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const cf lo = tr[r], hi = tr[r + 16];
-                        const cf u = h2 ? csub(lo, hi) : cadd(lo, hi);
+                        const cf u = cmk(fmaf(sg, hi.x, lo.x), fmaf(sg, hi.y, lo.y));
                         v[r] = h2 ? cmul(u, cmk(Rot32::c[r], Rot32::s[r])) : u;
                     }
                 } else {
