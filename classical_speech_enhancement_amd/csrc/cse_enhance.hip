@@ -198,16 +198,23 @@ struct WG {
     static constexpr int OFF_G = OFF_Y + 2 * YROW;                // float[2][B]
     static constexpr int OFF_C = OFF_G + 2 * GROW;                // float[2][HMAX]
     static constexpr int CBUF = 2 * HMAX * 4;
-    // n_fft 1024 halves two tables: the pass-1 twiddles keep the 16 lane
-    // residues b2, since e^{2πi (b2 + 16 h2) b/M} = tw[b][b2] W32^{h2 b}; the
-    // window keeps slots q < 16, since slot q + 16 is n + N/2 and
-    // w(n + N/2) = 1 - w(n)
+    // n_fft 1024 keeps two tables small.  The window keeps slots q < 16, since
+    // slot q + 16 is n + N/2 and w(n + N/2) = 1 - w(n) (the full 32-slot table
+    // fits the LDS budget once the twiddles shrink, but measured 64.9 vs
+    // 57.4 ms at 13 pairs).  The pass-1 twiddles come from two rotors per
+    // lane, e^{2πi i/M} and e^{2πi 4i/M} (16 B): tw_b = r1^(b mod 4) r4^(b div 4),
+    // 13 complex products, at most three roundings deep.  That replaced a
+    // 16-column table (keyed by b2, times W32^{h2 b} and a select on the other
+    // half of the lanes): -35 VALU and 7 of 8 LDS reads per frame, 58.2 ->
+    // 57.4 ms at 13 pairs.  n_fft 512 reads the full table (8 ds_read_b128).
     static constexpr bool HALF_TABLES = (NFFT == 1024);
-    static constexpr int TWL = HALF_TABLES ? 16 : G::L;          // twiddle columns
-    // pass-1 twiddles: one row of 18 complex (144 B) per column, entry b - 1:
-    // the ds_read_b128 of a 16-lane group hit disjoint banks
-    static constexpr int OFF_TW = OFF_C + CBUF;                   // cf[TWL][18]
-    static constexpr int OFF_LC = OFF_TW + TWL * 144;             // cf[L] packing rotor
+    static constexpr bool ROTOR_TW = (NFFT == 1024);
+    static constexpr int TWL = G::L;                              // twiddle columns (table form)
+    // pass-1 twiddles (512): one row of 18 complex (144 B) per column, entry
+    // b - 1: the ds_read_b128 of a 16-lane group hit disjoint banks;
+    // (1024): cf[L][2] rotors
+    static constexpr int OFF_TW = OFF_C + CBUF;
+    static constexpr int OFF_LC = OFF_TW + (ROTOR_TW ? G::L * 16 : TWL * 144);  // cf[L] packing rotor
     static constexpr int OFF_CP = OFF_LC + G::L * 8;              // float[CPWG][8]
     // synthesis window w(n)/NFFT at the lane's 32 (16) sample slots; row stride
     // 36 (20) floats: the lanes of a ds_read_b128 group hit disjoint banks
@@ -401,11 +408,20 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 
     // ---- workgroup tables: pass-1 twiddles e^{2πi i b/M} [b-1][i], lane
     // constants [i], cell parameters [slot]
-    for (int e = tid; e < 15 * W::TWL; e += W::THREADS) {
-        const int b = 1 + e % 15, ii = e / 15;
-        double s, c;
-        sincospi(2.0 * (double)(ii * b) / (double)M, &s, &c);
-        ((cf*)(smem + W::OFF_TW))[ii * 18 + b - 1] = cmk((float)c, (float)s);
+    if constexpr (W::ROTOR_TW) {
+        for (int e = tid; e < 2 * L; e += W::THREADS) {
+            const int ii = e >> 1, b = (e & 1) ? 4 : 1;
+            double s, c;
+            sincospi(2.0 * (double)(ii * b) / (double)M, &s, &c);
+            ((cf*)(smem + W::OFF_TW))[e] = cmk((float)c, (float)s);
+        }
+    } else {
+        for (int e = tid; e < 15 * W::TWL; e += W::THREADS) {
+            const int b = 1 + e % 15, ii = e / 15;
+            double s, c;
+            sincospi(2.0 * (double)(ii * b) / (double)M, &s, &c);
+            ((cf*)(smem + W::OFF_TW))[ii * 18 + b - 1] = cmk((float)c, (float)s);
+        }
     }
     // lane tables: packing rotor e^{2πi ii/NFFT}; window w(n)/NFFT at the lane's sample slots q
     // (n = SP*(q>>1) + off + (q&1)); for 512/256 the reciprocal closed-form wss
@@ -555,9 +571,24 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 
             CSE_MARK("pass1");
             {
+                if constexpr (W::ROTOR_TW) {
+                    // twiddles e^{2πi i b/M} = r1^(b mod 4) r4^(b div 4) from the lane's
+                    // two rotors (one ds_read_b128; at most 3 roundings deep)
+                    const float4 q4 = *(const float4*)(smem + W::OFF_TW + 16 * i);
+                    const cf r1 = cmk(q4.x, q4.y), r4 = cmk(q4.z, q4.w);
+                    idft16(z);
+                    const cf r2 = cmul(r1, r1), r8 = cmul(r4, r4);
+                    const cf lo[4] = {cmk(1.0f, 0.0f), r1, r2, cmul(r2, r1)};
+                    const cf hi[4] = {cmk(1.0f, 0.0f), r4, r8, cmul(r8, r4)};
+#pragma unroll
+                    for (int b = 1; b < 16; ++b) {
+                        const cf t = (b & 3) == 0 ? hi[b >> 2] : (b < 4 ? lo[b] : cmul(lo[b & 3], hi[b >> 2]));
+                        z[b] = cmul(z[b], t);
+                    }
+                } else {
                 // pass-1 twiddles e^{2πi i' b/M}, b = 1..15, of my column (per-lane
                 // row of 18 complex: 8 ds_read_b128), issued ahead of the DFT
-                const float4* twr = (const float4*)(smem + W::OFF_TW + 144 * ((L == 16) ? i : b2));
+                const float4* twr = (const float4*)(smem + W::OFF_TW + 144 * i);
                 float4 t4[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) t4[k] = twr[k];
@@ -566,12 +597,8 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 for (int b = 1; b < 16; ++b) {
                     const float4 q4 = t4[(b - 1) >> 1];
                     const cf t = ((b - 1) & 1) ? cmk(q4.z, q4.w) : cmk(q4.x, q4.y);
-                    if constexpr (W::HALF_TABLES) {  // column i = b2 + 16 h2: x W32^{h2 b}
-                        const cf th = cmul(t, cmk(Rot32::c[b], Rot32::s[b]));
-                        z[b] = cmul(z[b], h2 ? th : t);
-                    } else {
-                        z[b] = cmul(z[b], t);
-                    }
+                    z[b] = cmul(z[b], t);
+                }
                 }
             }
             CSE_MARK("pass2");
