@@ -13,11 +13,21 @@ quarter that are exact duplicates (min_tracking ignores noise_percentile).
 
 Scaling modes (one process per GPU under torchrun, RCCL = backend "nccl"):
   default  --pairs-total 100: BASELINE config 4's fixed job of 100 pairs,
-           cells sharded over the ranks by search.assign_lpt (the sweep
-           driver's greedy LPT over (pair, n_fft, hop, algorithm) items);
+           cells sharded over the ranks by search.assign_shards (contiguous
+           runs of cell ids of equal modelled cost: whole pairs per rank);
            "scaling": "strong", value = 100 pairs' units / max-rank time.
   --pairs P: P pairs per GPU ("scaling": "weak").
 Every step ends with one all_gather_into_tensor of the per-cell records.
+
+The line also carries two labelled blocks beside the headline:
+  full_grid     the same step over the whole HEAD grid, both n_fft halves
+                (9,744 cells per pair), with each half's kernel time;
+  sweep         the reference's whole job through search.run_grid: alignment,
+                SNR and STOI of every cell, the gather and both sequential
+                selections, wall seconds and cells/s;
+and "roofline", the enhance kernel against VALU issue (the resource it
+spends), with the measured HBM GB/s and SURVEY §8(d)'s algorithmic byte
+figure beside it.
 
 At N = 1 the line also carries
   parity        the timed step's per-cell SNR table of pair 0 against the
@@ -28,6 +38,7 @@ At N = 1 the line also carries
   cpu_baseline  the oracle on this host's cores (see cpu_baseline()).
 
     python bench.py [--gpus N --steps K --warmup W --pairs-total 100 | --pairs P]
+                    [--full-grid-steps F] [--no-sweep]
 """
 
 import argparse
@@ -170,7 +181,8 @@ def cpu_run(budget_s, seconds, n_fft, y_cells, timed=True):
 def load_pmc(units_per_launch, n_fft):
     """Counters of the enhance kernel for this exact launch size and n_fft,
     from the committed rocprofv3 PMC passes (profiles/pmc_*.json,
-    tools/pmc_summary.py; the newest round wins)."""
+    tools/pmc_summary.py; the newest round wins; roofline_block uses them only
+    while their kernel_src_sha matches this build's)."""
     import glob
     best = None
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
@@ -182,6 +194,175 @@ def load_pmc(units_per_launch, n_fft):
                 and (best is None or str(d.get("round", "")) >= str(best.get("round", "")))):
             best = d
     return best
+
+
+def kernel_src_sha():
+    """Digest of the enhance kernel's sources and build flags: a committed PMC
+    profile counts the instructions of one binary, so bench.py uses its
+    counters only while this digest matches the one the profile recorded."""
+    import hashlib
+    import __graft_entry__ as ge
+    h = hashlib.sha256()
+    for f in ("cse_enhance.hip", "cse_enhance_512.hip", "cse_enhance_1024.hip", "cse_common.hpp",
+              "cse_special.hpp"):
+        h.update(open(os.path.join(ge.CSRC, f), "rb").read())
+    h.update(open(os.path.join(REPO, "include", "cse.h"), "rb").read())
+    h.update(repr(sorted(ge.OWN_FLAGS.items())).encode())
+    return h.hexdigest()[:16]
+
+
+def rank_job(args, world, rank, n_fft):
+    """(pair ids of this rank, its cell specs as (slot, algorithm, params),
+    their global cell ids, units of the whole job per step, pairs in the whole
+    job).  n_fft None: the full grid (both halves)."""
+    from classical_speech_enhancement_amd import search
+    from classical_speech_enhancement_amd.engine import n_frames
+    L = int(round(args.seconds * 16000))
+    if args.pairs is not None:   # weak: P pairs per rank
+        total_pairs = args.pairs * world
+        pair_ids = [rank * args.pairs + i for i in range(args.pairs)]
+        local = [tuple(s) for s in search.job_specs(args.pairs, n_fft=n_fft)]
+        gids = rank * len(local) + np.arange(len(local), dtype=np.int64)
+    else:                        # strong: the fixed job, contiguous cost-balanced shards
+        total_pairs = args.pairs_total
+        specs = search.job_specs(total_pairs, n_fft=n_fft)
+        rank_of, _ = search.assign_shards(specs, [L] * total_pairs, world)
+        mine = np.flatnonzero(rank_of == rank)
+        pair_ids = sorted(set(specs.pair[mine].tolist()))
+        slot = {p: s for s, p in enumerate(pair_ids)}
+        local = [(slot[int(specs.pair[c])],) + tuple(specs[int(c)])[1:] for c in mine]
+        gids = mine.astype(np.int64)
+    units = sum(n_frames(L, p["hop_length"]) for (_, _, p) in grid_specs(1, n_fft)) * total_pairs
+    return pair_ids, local, gids, units, total_pairs
+
+
+class TimedJob:
+    """A rank's share of one step's work — STFT + noise PSDs, the fused enhance
+    of every cell (one launch per n_fft), one all_gather of the per-cell records
+    — over device-resident pairs.  Two plan sets alternate: the next step's
+    analysis runs on a side stream under this step's enhance (no data shared)."""
+
+    def __init__(self, eng, noisy, clean, specs, gids, n_buf, align, dist_ctx):
+        import torch
+        self.torch = torch
+        S, L = noisy.shape
+        self.noisy, self.clean, self.align = noisy, clean, align
+        self.dist, self.coll_dev, self.world = dist_ctx
+        self.n_buf = n_buf
+        self.mps = [eng.plan(S, L, specs, with_clean=True, align=align) for _ in range(n_buf)]
+        self.units = self.mps[0].units
+        self.main_s = torch.cuda.current_stream()
+        self.prep_s = torch.cuda.Stream() if n_buf > 1 else self.main_s
+        self.ev_prep = [torch.cuda.Event() for _ in range(n_buf)]
+        self.ev_done = [None] * n_buf
+        self.k = 0
+        n_rec = sum(p.n_packed for p in self.mps[0].plans)
+        if self.dist is not None:
+            t = torch.tensor([n_rec], dtype=torch.int64, device=self.coll_dev)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            n_rec = int(t.item())
+        # records: sse, finite, global cell id (-1: padding slot) per packed slot
+        self.rec_pad = torch.zeros((3, n_rec), dtype=torch.float64, device="cuda")
+        self.rec_pad[2] = -1.0
+        o = 0
+        for p in self.mps[0].plans:  # every plan set packs alike
+            real = p.order >= 0
+            g = np.full(p.n_packed, -1, dtype=np.int64)
+            g[real] = np.asarray(gids, dtype=np.int64)[p.idx[p.order[real]]]
+            self.rec_pad[2, o:o + p.n_packed] = torch.as_tensor(g.astype(np.float64))
+            o += p.n_packed
+        self.rec_all = torch.empty((self.world * 3, n_rec), dtype=torch.float64,
+                                   device=self.coll_dev)
+        self.gathered = None
+        if n_buf > 1:
+            self.prep(0)
+
+    def prep(self, k):
+        b = k % self.n_buf
+        torch = self.torch
+        with torch.cuda.stream(self.prep_s):
+            if self.ev_done[b] is not None:
+                self.prep_s.wait_event(self.ev_done[b])  # the enhance that last read these buffers
+            for p in self.mps[b].plans:
+                p.prepare(self.noisy, self.clean)
+            self.ev_prep[b].record(self.prep_s)
+
+    def step(self, evs=None):
+        """evs: per plan (start, end) timing events around its enhance launch."""
+        torch = self.torch
+        b = self.k % self.n_buf
+        self.k += 1
+        mp = self.mps[b]
+        if self.n_buf == 1:
+            self.prep(self.k - 1)
+        self.main_s.wait_event(self.ev_prep[b])
+        for j, plan in enumerate(mp.plans):
+            if evs is not None:
+                evs[j][0].record()
+            plan.enhance()
+            if evs is not None:
+                evs[j][1].record()
+            if self.align:
+                plan.finalize()
+        self.ev_done[b] = torch.cuda.Event()
+        self.ev_done[b].record(self.main_s)
+        if self.n_buf > 1:
+            self.prep(self.k)  # overlaps this step's enhance (the timed region holds K preps)
+        o = 0
+        for plan in mp.plans:
+            m = plan.n_packed
+            self.rec_pad[0, o:o + m] = plan.sse_d
+            self.rec_pad[1, o:o + m] = plan.fin_d
+            o += m
+        if self.dist is not None:
+            self.dist.all_gather_into_tensor(self.rec_all, self.rec_pad.to(self.coll_dev))
+            self.gathered = self.rec_all.cpu()
+        else:
+            self.gathered = self.rec_pad.cpu()
+        return self.gathered
+
+    def table(self, n_cells):
+        """The last step's gathered records as [n_cells, 2] (sse, finite) by
+        global cell id; every cell exactly once."""
+        r = self.gathered.numpy().reshape(self.world, 3, -1).transpose(1, 0, 2).reshape(3, -1)
+        ids = r[2].astype(np.int64)
+        keep = ids >= 0
+        ids = ids[keep]
+        assert len(ids) == n_cells and len(np.unique(ids)) == n_cells, "gathered records"
+        out = np.empty((n_cells, 2))
+        out[ids, 0] = r[0][keep]
+        out[ids, 1] = r[1][keep]
+        return out
+
+    def run(self, steps, warmup):
+        """Warmup, then K timed steps bracketed by barrier + synchronize; returns
+        (seconds, max over ranks; mean enhance-kernel ms per plan)."""
+        torch = self.torch
+        for _ in range(warmup):
+            self.step()
+        torch.cuda.synchronize()
+        n_pl = len(self.mps[0].plans)
+        evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(n_pl)] for _ in range(steps)]
+        if self.dist is not None:
+            self.dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            self.step(evs[k])
+        torch.cuda.synchronize()
+        if self.dist is not None:
+            self.dist.barrier()
+        dt = time.perf_counter() - t0
+        if self.dist is not None:
+            t = torch.tensor([dt], dtype=torch.float64, device=self.coll_dev)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            dt = float(t.item())
+        kern = [float(np.mean([e[j][0].elapsed_time(e[j][1]) for e in evs])) for j in range(n_pl)]
+        return dt, kern
+
+    def last_plans(self):
+        return self.mps[(self.k - 1) % self.n_buf].plans
 
 
 def main():
@@ -205,6 +386,14 @@ def main():
     ap.add_argument("--align", action="store_true",
                     help="also run finalize_enhanced's alignment (xcorr lag + lag-shifted rescoring)"
                          " inside the step (SURVEY §8(f) row 1; not part of the §8(d) timed region)")
+    ap.add_argument("--full-grid-steps", type=int, default=None,
+                    help="timed steps of the full_grid block (both n_fft halves; default "
+                         "min(steps, 5)); 0 skips the block")
+    ap.add_argument("--dump-table", default=None,
+                    help="rank 0 saves the last timed step's gathered records [cells, 2] "
+                         "(sse, finite) by global cell id to this .npy (multi-rank tests)")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="skip the sweep block (search.run_grid with alignment and STOI)")
     args = ap.parse_args()
 
     import torch
@@ -218,121 +407,64 @@ def main():
         # multi-rank path with several ranks sharing one GPU (1-GPU boxes)
         dist.init_process_group(os.environ.get("CSE_DIST_BACKEND", "nccl"))
     torch.cuda.set_device(local % torch.cuda.device_count())
-    from classical_speech_enhancement_amd import search
-    from classical_speech_enhancement_amd.engine import Engine, n_frames, snr_db
+    from classical_speech_enhancement_amd.engine import Engine, snr_db
     from classical_speech_enhancement_amd.synth import make_pair
     nccl = use_dist and dist.get_backend() == "nccl"
     coll_dev = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
+    dist_ctx = (dist if use_dist else None, coll_dev, world)
+    weak = args.pairs is not None
 
-    L = int(round(args.seconds * 16000))
-    if args.pairs is not None:   # weak: P pairs per rank
-        weak = True
-        pair_ids = [rank * args.pairs + i for i in range(args.pairs)]
-        local_specs = grid_specs(args.pairs, args.nfft)
-        total_pairs = args.pairs * world
-    else:                        # strong: the fixed job, cells sharded by LPT
-        weak = False
-        total_pairs = args.pairs_total
-        all_specs = grid_specs(total_pairs, args.nfft)
-        rank_of, _ = search.assign_lpt(all_specs, [L] * total_pairs, world)
-        mine = np.nonzero(rank_of == rank)[0]
-        pair_ids = sorted({all_specs[c][0] for c in mine})
-        slot = {p: s for s, p in enumerate(pair_ids)}
-        local_specs = [(slot[all_specs[c][0]], all_specs[c][1], all_specs[c][2]) for c in mine]
-    total_units = sum(n_frames(L, p["hop_length"]) for p in
-                      (s[2] for s in grid_specs(1, args.nfft))) * total_pairs
-
+    pair_ids, local_specs, gids, total_units, total_pairs = rank_job(args, world, rank, args.nfft)
     eng = Engine()
     pairs = [make_pair(i, args.seconds) for i in pair_ids]
     clean = torch.as_tensor(np.stack([c for c, _ in pairs])).cuda()
     noisy = torch.as_tensor(np.stack([n for _, n in pairs])).cuda()
     clean_pow = np.array([float(np.dot(c, c)) for c, _ in pairs])
-    # Two plans, double-buffered: the next step's STFT + noise PSDs run on a
-    # side stream while this step's enhance kernel runs (no data is shared
-    # between a step's prep and the previous step's enhance).
-    n_buf = 1 if args.no_overlap else 2
-    mps = [eng.plan(len(pairs), L, local_specs, with_clean=True, align=args.align)
-           for _ in range(n_buf)]
-    plans = [m.plans[0] for m in mps]
-    units = mps[0].units
-    main_s = torch.cuda.current_stream()
-    prep_s = torch.cuda.Stream() if n_buf > 1 else main_s
-    ev_prep = [torch.cuda.Event() for _ in range(n_buf)]
-    ev_done = [None] * n_buf
-    counter = [0]
-    # records of every rank, padded to the largest shard: one all_gather per step
-    n_rec = plans[0].n_packed
-    if use_dist:
-        t = torch.tensor([n_rec], dtype=torch.int64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        n_rec = int(t.item())
-    rec_pad = torch.zeros((2, n_rec), dtype=torch.float64, device="cuda")
-    rec_all = torch.empty((world * 2, n_rec), dtype=torch.float64, device=coll_dev)
-
-    def prep(k):
-        b = k % n_buf
-        with torch.cuda.stream(prep_s):
-            if ev_done[b] is not None:
-                prep_s.wait_event(ev_done[b])  # the enhance that last read these buffers
-            plans[b].prepare(noisy, clean)
-            ev_prep[b].record(prep_s)
-
-    def step(ev=None):
-        k = counter[0]
-        counter[0] += 1
-        b = k % n_buf
-        plan = plans[b]
-        if n_buf == 1:
-            prep(k)
-        main_s.wait_event(ev_prep[b])
-        if ev is not None:
-            ev[0].record()
-        plan.enhance()
-        if ev is not None:
-            ev[1].record()
-        if args.align:
-            plan.finalize()
-        ev_done[b] = torch.cuda.Event()
-        ev_done[b].record(main_s)
-        if n_buf > 1:
-            prep(k + 1)  # overlaps this step's enhance (the timed region holds K preps)
-        m = plan.n_packed
-        rec_pad[0, :m] = plan.sse_d
-        rec_pad[1, :m] = plan.fin_d
-        if use_dist:
-            dist.all_gather_into_tensor(rec_all, rec_pad.to(coll_dev))
-            return rec_all.cpu()
-        return rec_pad.cpu()
-
-    if n_buf > 1:
-        prep(0)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(events[k])
-    torch.cuda.synchronize()
-    if use_dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if use_dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    job = TimedJob(eng, noisy, clean, local_specs, gids, 1 if args.no_overlap else 2,
+                   args.align, dist_ctx)
+    units = job.units
+    dt, kern = job.run(args.steps, args.warmup)
+    kern_ms = kern[0]
+    n_cells_job = len(grid_specs(1, args.nfft)) * total_pairs
+    table = job.table(n_cells_job)
+    if args.dump_table and rank == 0:
+        np.save(args.dump_table, table)
 
     # sanity of the step's output: every cell finite, SNRs finite
-    last = plans[(counter[0] - 1) % n_buf]
-    sse, fin = last.results()[:2]
+    sse, fin = job.last_plans()[0].results()[:2]
     assert fin.all(), "non-finite enhanced output"
     snr_local = snr_db(sse, clean_pow[[s for (s, _, _) in local_specs]])
     assert np.isfinite(snr_local).all()
+    del job
+
+    # ---- full_grid: both n_fft halves of the HEAD grid per step (9,744 cells per pair)
+    full = None
+    fsteps = min(args.steps, 5) if args.full_grid_steps is None else args.full_grid_steps
+    if fsteps > 0:
+        f_ids, f_specs, f_gids, f_units, _ = rank_job(args, world, rank, None)
+        f_pairs = [make_pair(i, args.seconds) for i in f_ids]
+        f_clean = torch.as_tensor(np.stack([c for c, _ in f_pairs])).cuda()
+        f_noisy = torch.as_tensor(np.stack([n for _, n in f_pairs])).cuda()
+        fjob = TimedJob(eng, f_noisy, f_clean, f_specs, f_gids, 1 if args.no_overlap else 2,
+                        False, dist_ctx)
+        fdt, fkern = fjob.run(fsteps, 1)
+        full = {"what": ("the whole HEAD grid per step: both n_fft halves (9,744 cells per pair, "
+                         "all 4 algorithms, hops 128+256), STFT + noise PSDs + fused "
+                         "gain/ISTFT/SNR per cell, records all-gathered; same sharding and timing "
+                         "rules as the headline"),
+                "value": f_units * fsteps / fdt, "unit": "frame-gain evals/s",
+                "units_per_step": f_units, "cells_per_step": 9744 * total_pairs,
+                "steps": fsteps, "warmup": 1, "ms_per_step": fdt / fsteps * 1e3,
+                "kernel_ms": {str(p.n_fft): k for p, k in zip(fjob.mps[0].plans, fkern)},
+                "units_per_launch_rank0": {str(p.n_fft): p.units for p in fjob.mps[0].plans}}
+        del fjob, f_clean, f_noisy
+
+    # ---- sweep: the reference's whole job (speech_enhancement_comparison.py:441-455 ->
+    # :156-226) through search.run_grid: every cell aligned, SNR and STOI scored,
+    # records gathered, both sequential selections
+    sweep = None
+    if not args.no_sweep:
+        sweep = sweep_block(args, world, total_pairs, weak)
 
     if rank != 0:
         if use_dist:
@@ -340,33 +472,6 @@ def main():
             dist.destroy_process_group()
         return
     value = total_units * args.steps / dt
-    bytes_per_unit = 12 * (args.nfft // 2 + 1)
-    achieved = units * bytes_per_unit / (kern_ms / 1e3)
-    pmc = load_pmc(units, args.nfft)
-    roof = {
-        "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-        "frac": achieved / HBM_PEAK, "traffic": None,
-        "kernel": f"cse::enhance_kernel<{args.nfft}>", "kernel_ms": kern_ms,
-        "bytes_per_unit": bytes_per_unit, "units_per_launch": units,
-        "note": ("frac is SURVEY §8(d)'s algorithmic-byte roofline (12 B per bin per unit). "
-                 "The kernel is fused: its HBM traffic ('traffic', PMC) is a few % of those "
-                 "bytes, and VALU issue ('valu') is the resource it actually spends"),
-    }
-    if pmc:
-        roof["traffic"] = pmc.get("hbm_bytes_per_launch")
-        vi, tr = pmc.get("sq_insts_valu"), pmc.get("sq_insts_valu_trans")
-        if vi:
-            need = VALU_CYC * (vi - (tr or 0)) + TRANS_CYC * (tr or 0)  # SIMD issue cycles
-            v = {"insts_valu": vi, "insts_trans": tr, "issue_cycles": need,
-                 "frac_at_2p4ghz": need / (SIMDS * CLOCK * kern_ms / 1e3),
-                 "cycles_per": f"VALU {VALU_CYC}, transcendental {TRANS_CYC} per wave64 per SIMD",
-                 "source": pmc.get("source")}
-            busy = pmc.get("sq_busy_cycles")
-            if busy:  # per-SE cycles with waves resident (summed over 32 SEs): the clock held
-                cyc = busy / 32
-                v["clock_ghz"] = cyc / (pmc["kernel_ms"] / 1e3) / 1e9
-                v["frac"] = need / (SIMDS * cyc)
-            roof["valu"] = v
     res = {
         "metric": METRIC,
         "value": value,
@@ -378,25 +483,31 @@ def main():
         "higher_is_better": True,
         "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": ("f32 gain recursion + ISTFT + per-frame error sums; f64 STFT, noise PSDs, "
+                  "cross-frame SNR sums, alignment re-evaluation and STOI"),
         "data": "synthetic",
         "config": {
             "workload": (f"{total_pairs} x 10-s 16-kHz synthetic pairs "
-                         f"({'per GPU' if weak else 'in all, cells sharded over the GPUs by LPT'})"
+                         f"({'per GPU' if weak else 'in all, cells sharded over the GPUs'})"
                          f", HEAD parameter_ranges.py grid at n_fft={args.nfft} (all 4 algorithms, "
                          f"4872 cells/pair, hops 128+256): STFT + noise PSDs + fused "
                          f"gain/ISTFT/SNR per cell, records all-gathered"),
             "pairs_total": total_pairs, "clip_s": args.seconds, "sr": 16000, "n_fft": args.nfft,
-            "cells_total": len(grid_specs(1, args.nfft)) * total_pairs,
+            "cells_total": n_cells_job,
+            "gathered_cells_finite": int(table[:, 1].sum()),
             "units_per_step": total_units, "units_per_step_rank0": units,
             "pairs_rank0": len(pair_ids),
-            "parallelism": (f"{'pairs' if weak else 'LPT cell shards'} over {world} rank(s), "
-                            f"one all_gather_into_tensor of per-cell records per step "
-                            f"({'RCCL' if nccl else ('gloo' if use_dist else 'single process')})"),
+            "parallelism": (f"{'pairs' if weak else 'contiguous cost-balanced cell shards'} over "
+                            f"{world} rank(s), one all_gather_into_tensor of per-cell records per "
+                            f"step ({'RCCL' if nccl else ('gloo' if use_dist else 'single process')})"),
             "finalize_alignment": bool(args.align),
         },
-        "roofline": roof,
+        "roofline": roofline_block(args.nfft, units, kern_ms),
     }
+    if full is not None:
+        res["full_grid"] = full
+    if sweep is not None:
+        res["sweep"] = sweep
     if world == 1:
         # pair 0 is the CPU's pair: its grid is this plan's first cells
         y_cells = [] if args.no_parity else parity_cells(args.seconds, args.nfft)
@@ -416,6 +527,118 @@ def main():
         dist.destroy_process_group()
     if "parity" in res and not res["parity"]["pass"]:
         sys.exit("parity check failed: " + json.dumps(res["parity"]))
+
+
+def roofline_block(n_fft, units, kern_ms):
+    """The enhance kernel against the resource it spends: VALU issue.
+
+    achieved = the launch's SIMD issue cycles (PMC instruction counts of this
+    binary and launch: VALU 2 cycles per wave64, transcendental 4, fp64 FMA/MUL/
+    ADD 4) / the live HIP-event kernel time; peak = 1024 SIMDs x 2.4 GHz.
+    frac_at_held_clock uses the clock the profiled run held instead.  Beside
+    it: the measured HBM traffic (PMC) as GB/s and SURVEY §8(d)'s algorithmic
+    12 B/bin figure, which a fused kernel does not move."""
+    bytes_per_unit = 12 * (n_fft // 2 + 1)
+    ks = kern_ms / 1e3
+    alg = units * bytes_per_unit / ks
+    roof = {"bound": "valu", "achieved": None, "peak": SIMDS * CLOCK / 1e9,
+            "unit": "G SIMD issue-cycles/s (1024 SIMDs)", "frac": None, "traffic": None,
+            "kernel": f"cse::enhance_kernel<{n_fft}>", "kernel_ms": kern_ms,
+            "units_per_launch": units,
+            "hbm_algorithmic_GBps": alg / 1e9, "hbm_algorithmic_frac": alg / HBM_PEAK,
+            "bytes_per_unit_algorithmic": bytes_per_unit,
+            "hbm_measured_GBps": None, "hbm_measured_frac": None,
+            "kernel_src_sha": kernel_src_sha()}
+    pmc = load_pmc(units, n_fft)
+    if not pmc:
+        roof["note"] = "no committed PMC profile for this launch size: VALU figures absent"
+        return roof
+    roof["pmc_source"] = pmc.get("source")
+    roof["pmc_matches_build"] = pmc.get("kernel_src_sha") == roof["kernel_src_sha"]
+    if not roof["pmc_matches_build"]:
+        roof["note"] = ("the committed PMC profile was taken on other kernel sources: "
+                        "VALU and traffic figures omitted")
+        return roof
+    tb = pmc.get("hbm_bytes_per_launch")
+    if tb:
+        roof["traffic"] = tb
+        roof["hbm_measured_GBps"] = tb / ks / 1e9
+        roof["hbm_measured_frac"] = tb / ks / HBM_PEAK
+    need = pmc.get("valu_issue_cycles")
+    if need:
+        roof["achieved"] = need / ks / 1e9
+        roof["frac"] = need / ks / (SIMDS * CLOCK)
+        roof["issue_cycles_per_launch"] = need
+        roof["cycles_per"] = ("wave64 VALU 2, transcendental 4 (tools/micro/valu_rate.hip), "
+                              "fp64 FMA/MUL/ADD 4 per SIMD")
+        if pmc.get("clock_ghz_profiled"):
+            roof["clock_ghz_profiled"] = pmc["clock_ghz_profiled"]
+            roof["frac_at_held_clock"] = pmc.get("valu_frac")
+        for k in ("share_wait_inst_any", "lds_conflict_cycles_per_lds_inst", "vgprs"):
+            if pmc.get(k) is not None:
+                roof[k] = pmc[k]
+    return roof
+
+
+def sweep_block(args, world, total_pairs, weak):
+    """search.run_grid over the whole job: pairs x 9,744 cells, alignment + SNR
+    + STOI, one all_gather, sequential selections.  One warm call (plans
+    allocated), then one timed call bracketed by barrier + synchronize, max over
+    ranks."""
+    import torch
+    import torch.distributed as dist
+    from classical_speech_enhancement_amd import search
+    from classical_speech_enhancement_amd.engine import Engine
+    from classical_speech_enhancement_amd.synth import make_pair
+    pairs = [make_pair(i, args.seconds) for i in range(total_pairs)]
+    clean = [c for c, _ in pairs]
+    noisy = [n for _, n in pairs]
+    specs = search.job_specs(total_pairs)
+    seng = Engine()
+    seng.plan_cache_size = 2  # the STOI path's two alternating plans stay cached between calls
+
+    def compute(c, n, s, ids):
+        return search.engine_compute(c, n, s, ids, engine=seng)
+    use_dist = dist.is_available() and dist.is_initialized()
+    search.run_grid(clean, noisy, specs, compute=compute)  # warm: plans allocated
+    if use_dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    table, best = search.run_grid(clean, noisy, specs, compute=compute)
+    best_stoi = search.select_best(specs, table, "stoi")
+    torch.cuda.synchronize()
+    if use_dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if use_dist:
+        t = torch.tensor([dt], dtype=torch.float64)
+        if dist.get_backend() == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    L = int(round(args.seconds * 16000))
+    units = sum(1 + L // int(p["hop_length"]) for (_, _, p) in specs[:specs.per_pair]) * total_pairs
+    st = table[:, 5].astype(np.int64)
+    out = {"what": ("search.run_grid over the whole job (speech_enhancement_comparison.py:"
+                    "441-455 -> 156-226): STFT, noise PSDs, fused enhance of every cell, "
+                    "finalize_enhanced alignment (xcorr lag, lag-shifted rescoring), SNR and "
+                    "STOI of every cell, one all_gather of the records, the sequential SNR "
+                    "and STOI selections; host-resident pairs in, winners out (second call: "
+                    "device plans reused)"),
+           "pairs": total_pairs, "cells": len(specs), "units": units, "wall_s": dt,
+           "cells_per_s": len(specs) / dt, "units_per_s": units / dt,
+           "cells_computed": "min_tracking cells that differ only in noise_percentile are "
+                             "computed once and their rows copied (a quarter of the grid)",
+           "finite_cells": int(table[:, 2].sum()),
+           "xcorr_status": {"ok": int((st == 0).sum()), "flat": int((st == 1).sum()),
+                            "nonfinite": int((st == 2).sum())},
+           "nonzero_lags": int((table[:, 4] != 0).sum()),
+           "winners": {"snr": sum(1 for v in best.values() if v[0] >= 0),
+                       "stoi": sum(1 for v in best_stoi.values() if v[0] >= 0),
+                       "groups": len(best)}}
+    del seng
+    return out
 
 
 def parity_block(eng, noisy, clean, clean_pow, n_fft, snr_local, cpu_snr, cpu_y, weak):

@@ -54,7 +54,7 @@ EXPORTS = ("cse_version", "cse_last_error", "cse_cells_per_group", "cse_stft",
            "cse_xcorr_workspace_bytes", "cse_xcorr_prepare", "cse_xcorr_lag",
            "cse_stoi_workspace_bytes", "cse_stoi_scratch_bytes", "cse_stoi_prepare",
            "cse_stoi_cells")
-XCORR_OK, XCORR_AMBIGUOUS, XCORR_NONFINITE = 0, 1, 2
+XCORR_OK, XCORR_FLAT, XCORR_NONFINITE = 0, 1, 2  # FLAT: slow exact path ran (lag exact)
 
 
 def cells_per_group(n_fft):

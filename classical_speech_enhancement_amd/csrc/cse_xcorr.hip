@@ -21,8 +21,9 @@
 // 1e-6 ||r0|| ||s0|| of the exact one, so every lag within
 // delta = 2e-5 ||r0|| ||s0|| of the fp32 maximum is re-evaluated by a direct
 // fp64 sum and the lag is chosen among those (ties -> smallest lag, like
-// np.argmax).  More than XCAND such candidates (a flat correlation) keeps the
-// fp32 argmax and reports status CSE_XCORR_AMBIGUOUS.
+// np.argmax).  The candidates are marked in an LDS bitmap over the lags and
+// re-evaluated in ascending lag order, however many there are; more than
+// XCAND of them (a flat correlation) only sets status CSE_XCORR_FLAT.
 #include "cse_common.hpp"
 
 #include <type_traits>
@@ -33,7 +34,9 @@ constexpr int XN = 8192;      // real transform length of one block correlation
 constexpr int XH = XN / 2;    // complex FFT length
 constexpr int XB = XN - 2 * 1600;  // output samples per block: the 0.1-s lags of 16 kHz fill XN
 constexpr int XT = 256;       // threads per workgroup
-constexpr int XCAND = 64;     // candidates re-evaluated in fp64
+constexpr int XCAND = 64;     // more fp64 candidates than this: status FLAT
+constexpr int XLAGS = 2 * ((XN - XB) / 2) + 1;  // most lags a cell has (max_lag <= 1600)
+constexpr int XWORDS = (XLAGS + 31) / 32;        // candidate bitmap words
 constexpr int XHP = XH + XH / 16;  // LDS FFT buffer, one pad slot after every 16 points
 // padded LDS index: the first Stockham pass stores 16 consecutive points per
 // lane (lane stride 16 x 8 B, a 32-way bank conflict unpadded; 17 x 8 B with
@@ -319,7 +322,7 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     __shared__ double red[XT];
     __shared__ float rv[XT];
     __shared__ int ri[XT];
-    __shared__ int cand[XCAND];
+    __shared__ unsigned cbits[XWORDS];  // candidate lags k, bit k & 31 of word k >> 5
     __shared__ int ncand;
     const int cell = blockIdx.x, tid = threadIdx.x;
     const int sig = a.sig_of[cell];
@@ -468,47 +471,54 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     const int kmax = ri[0];
     const float delta = (float)(2e-5 * sqrt(a.rnorm[sig] * snorm)) + 1e-30f;
     if (tid == 0) ncand = 0;
+    for (int w = tid; w < XWORDS; w += XT) cbits[w] = 0u;
     __syncthreads();
     for (int k = tid; k <= 2 * L; k += XT) {
         const cf z = buf[px(k >> 1)];
         const float v = ((k & 1) ? z.y : z.x) * (1.0f / XN) - (float)(mu * Ws[k]);
         if (v >= cmax - delta) {
-            const int slot = atomicAdd(&ncand, 1);
-            if (slot < XCAND) cand[slot] = k;
+            atomicOr(&cbits[k >> 5], 1u << (k & 31));
+            atomicAdd(&ncand, 1);
         }
     }
     __syncthreads();
     const int nc = ncand;
     int kbest = kmax;
-    int status = CSE_XCORR_OK;
-    if (nc > XCAND) {
-        status = CSE_XCORR_AMBIGUOUS;
-    } else if (nc > 1) {
-        // exact fp64 re-evaluation: c(l) = sum over the overlap of r0[m + l] (e[m] - mu)
+    const int status = nc > XCAND ? CSE_XCORR_FLAT : CSE_XCORR_OK;
+    if (nc > 1) {
+        // exact fp64 re-evaluation of every candidate, in ascending lag order
+        // (the bitmap words are read by every thread alike: uniform control
+        // flow around block_sum's barriers):
+        //   c(l) = sum over the overlap of r0[m + l] (e[m] - mu)
         const double* r0 = a.r0buf + (int64_t)sig * n;
         double bestd = -INFINITY;
         kbest = 0x7fffffff;
-        for (int ci = 0; ci < nc; ++ci) {
-            const int k = cand[ci];
-            const int l = k - L;
-            const int m0 = l < 0 ? -l : 0, m1 = l > 0 ? n - l : n;
-            double acc = 0.0;
-            for (int m = m0 + tid; m < m1; m += 8 * XT) {
-                double rv8[8], ev8[8];
+        const int nw = (2 * L + 1 + 31) >> 5;
+        for (int w = 0; w < nw; ++w) {
+            unsigned bits = cbits[w];
+            while (bits) {
+                const int k = 32 * w + __builtin_ctz(bits);
+                bits &= bits - 1u;
+                const int l = k - L;
+                const int m0 = l < 0 ? -l : 0, m1 = l > 0 ? n - l : n;
+                double acc = 0.0;
+                for (int m = m0 + tid; m < m1; m += 8 * XT) {
+                    double rv8[8], ev8[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {  // issue all 8 pairs of loads first
-                    const int mm = min(m + u * XT, m1 - 1);
-                    rv8[u] = r0[mm + l];
-                    ev8[u] = (double)e[mm];
+                    for (int u = 0; u < 8; ++u) {  // issue all 8 pairs of loads first
+                        const int mm = min(m + u * XT, m1 - 1);
+                        rv8[u] = r0[mm + l];
+                        ev8[u] = (double)e[mm];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (m + u * XT < m1) acc += rv8[u] * (ev8[u] - mu);
                 }
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (m + u * XT < m1) acc += rv8[u] * (ev8[u] - mu);
-            }
-            acc = block_sum(acc, red);
-            if (acc > bestd || (acc == bestd && k < kbest)) {
-                bestd = acc;
-                kbest = k;
+                acc = block_sum(acc, red);
+                if (acc > bestd) {  // ascending k: the first maximum is kept
+                    bestd = acc;
+                    kbest = k;
+                }
             }
         }
     }

@@ -270,7 +270,11 @@ class GridPlan:
 
     def __init__(self, eng, n_fft, S, L, items, with_clean, want_y, want_g, y_all=None,
                  align=False, true_len=None):
-        self.eng, self.n_fft, self.S, self.L = eng, n_fft, S, L
+        # the library and device only, not the Engine: the engine's plan cache
+        # holds this plan, and a back reference would make the pair a cycle
+        # that only the cyclic collector frees (with the plan's device buffers)
+        self.lib, self.device = eng.lib, eng.device
+        self.n_fft, self.S, self.L = n_fft, S, L
         self.true_len = L if true_len is None else int(true_len)
         if not 1 <= self.true_len <= L:
             raise ValueError(f"true_len={self.true_len} not in [1, {L}]")
@@ -403,8 +407,8 @@ class GridPlan:
 
     def prepare(self, noisy, clean=None):
         """Group-level analysis: STFTs and every noise row (once per signal batch)."""
-        eng, S, L, B = self.eng, self.S, self.L, self.B
-        lib = eng.lib
+        S, L, B = self.S, self.L, self.B
+        lib = self.lib
         st = _stream()
         for hop in self.hops:
             T = n_frames(L, hop)
@@ -462,7 +466,7 @@ class GridPlan:
             yo, olen = self.head, self.xc_n
         else:
             yo, olen = None, 0
-        _lib.check(self.eng.lib.cse_enhance_cells(
+        _lib.check(self.lib.cse_enhance_cells(
             self.n_fft, self.L, _ptr(self.cells_d), self.n_packed, _ptr(self.Ybuf),
             _ptr(self.pool), _ptr(self.clean), _ptr(yo), olen, _ptr(self.g_out),
             _ptr(self.sse_d), _ptr(self.fin_d), _stream()),
@@ -479,7 +483,7 @@ class GridPlan:
         (cse_xcorr_lag), then the cells whose lag is not 0 are scored again
         with the shifted output (cse_enhance_cells with cell.lag, plus the
         clean energy of the zero padding)."""
-        lib, st = self.eng.lib, _stream()
+        lib, st = self.lib, _stream()
         _lib.check(lib.cse_xcorr_prepare(_ptr(self.clean), self.S, self.L, self.xc_n,
                                          self.xc_lag_max, _ptr(self.xc_ws), st),
                    "cse_xcorr_prepare")
@@ -497,9 +501,9 @@ class GridPlan:
         cells["out_offset"] = -1
         cells["gain_offset"] = -1
         packed, order = pack_waves(cells, self.n_fft)
-        cd = torch.from_numpy(packed.view(np.uint8).copy()).to(self.eng.device)
-        sse = torch.zeros(len(packed), dtype=torch.float64, device=self.eng.device)
-        fin = torch.zeros(len(packed), dtype=torch.uint8, device=self.eng.device)
+        cd = torch.from_numpy(packed.view(np.uint8).copy()).to(self.device)
+        sse = torch.zeros(len(packed), dtype=torch.float64, device=self.device)
+        fin = torch.zeros(len(packed), dtype=torch.uint8, device=self.device)
         _lib.check(lib.cse_enhance_cells(
             self.n_fft, self.L, _ptr(cd), len(packed), _ptr(self.Ybuf), _ptr(self.pool),
             _ptr(self.clean), None, 0, None, _ptr(sse), _ptr(fin), st),

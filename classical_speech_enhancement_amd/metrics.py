@@ -82,10 +82,24 @@ class StoiPlan:
         if y.dtype != torch.float32 or not y.is_cuda:
             raise ValueError("y must be a float32 cuda tensor")
         if torch.is_tensor(y_offset):
+            # device indices: every check that needs no host synchronisation
+            # (the value ranges are the caller's; the kernel reads int64 / int32)
             off, sig = y_offset, sig_of
+            if not torch.is_tensor(sig):
+                raise ValueError("sig_of must be a cuda tensor when y_offset is one")
+            if off.dtype != torch.int64 or sig.dtype != torch.int32:
+                raise ValueError("device y_offset / sig_of must be int64 / int32")
+            if off.device != dev or sig.device != dev:
+                raise ValueError("device y_offset / sig_of must live on the clean signal's GPU")
+            if not (off.is_contiguous() and sig.is_contiguous()):
+                raise ValueError("device y_offset / sig_of must be contiguous")
             n = int(off.numel())
             if int(sig.numel()) != n:
                 raise ValueError("y_offset and sig_of differ in length")
+            if torch.is_tensor(lag) and (lag.dtype != torch.int32 or lag.device != dev
+                                         or not lag.is_contiguous() or int(lag.numel()) != n):
+                raise ValueError("device lag must be a contiguous int32 tensor of n entries "
+                                 "on the clean signal's GPU")
         else:
             off_h = np.asarray(y_offset, dtype=np.int64)
             sig_h = np.asarray(sig_of, dtype=np.int32)
@@ -100,8 +114,15 @@ class StoiPlan:
             sig = torch.as_tensor(sig_h, device=dev)
         lg = None
         if lag is not None:
-            lg = torch.as_tensor(np.asarray(lag, dtype=np.int32), device=dev) \
-                if not torch.is_tensor(lag) else lag.to(dev, torch.int32)
+            if torch.is_tensor(lag):
+                lg = lag.to(dev, torch.int32).contiguous()
+            else:
+                lag_h = np.asarray(lag, dtype=np.int32)
+                if len(lag_h) != n:
+                    raise ValueError("lag and y_offset differ in length")
+                lg = torch.as_tensor(lag_h, device=dev)
+            if int(lg.numel()) != n:
+                raise ValueError("lag and y_offset differ in length")
         if out is None:
             out = torch.empty(n, dtype=torch.float64, device=dev)
         for s in range(0, n, STOI_CHUNK):

@@ -10,9 +10,9 @@ Here the whole (pair x algorithm x grid cell) set is one job:
   work_items     cells grouped by what they share on the device:
                  (pair, n_fft, hop, algorithm) -> one STFT, one set of noise
                  rows; cost = cells x frames x bins x algorithm weight
-  assign_lpt     greedy longest-processing-time assignment of items to ranks
-                 (SURVEY §8(e)); an item larger than total/(2*world) is split
-                 in cell chunks first (splitting only repeats one STFT)
+  assign_shards  contiguous runs of cell ids of equal modelled cost per rank
+                 (SURVEY §8(e)'s cost model): whole pairs per rank, so each
+                 pair's STFT and noise PSDs run on one rank (two at a cut)
   run_grid       each rank computes its cells (Engine on its GPU), then ONE
                  all_gather of fixed-size records {cell_id, sse, snr, finite, stoi}
                  (RCCL over xGMI for backend "nccl", gloo in CPU tests)
@@ -47,8 +47,12 @@ ALGO_WEIGHT = {"spectralSubtractor": 1.0, "wiener": 1.1, "mmse": 2.0, "omlsa": 3
 # tolerance of the best-so-far update per objective (speech_enhancement_comparison.py:183,194,205)
 TOLERANCE = {"stoi": 1e-6, "pesq": 1e-3, "balance": 1e-5, "snr": 1e-5}
 
-RECORD_FIELDS = ("cell_id", "sse", "snr", "finite", "stoi")  # one float64 row per cell
-TABLE_COLUMN = {"sse": 0, "snr": 1, "finite": 2, "stoi": 3}  # table = records without cell_id
+# one float64 row per cell.  lag: finalize_enhanced's alignment lag (0 when
+# not aligned); xstatus: cse_xcorr_lag's status (engine: XCORR_OK, XCORR_FLAT =
+# the exact many-candidate path ran, XCORR_NONFINITE; 0 when not aligned)
+RECORD_FIELDS = ("cell_id", "sse", "snr", "finite", "stoi", "lag", "xstatus")
+TABLE_COLUMN = {"sse": 0, "snr": 1, "finite": 2, "stoi": 3, "lag": 4,
+                "xstatus": 5}  # table = records without cell_id
 NCOL = len(RECORD_FIELDS) - 1
 # bound on the cell waveforms held at once for STOI scoring (f32 bytes): 32 GB
 # of the 288 GB HBM, i.e. 5 full 10-s pairs (9,744 cells x 640 KB each) per batch
@@ -175,35 +179,50 @@ def work_items(specs, lengths):
     return items
 
 
-def assign_lpt(specs, lengths, world):
-    """Rank of every cell: items (split when > total/(2*world)) handed out
-    largest-first to the least-loaded rank (ties -> lowest rank)."""
-    items = work_items(specs, lengths)
-    total = sum(c for c, _ in items)
-    cap = total / (2.0 * world) if world > 1 else math.inf
-    pieces = []
-    for cost, ids in items:
-        n = max(1, int(math.ceil(cost / cap))) if cap < math.inf else 1
-        n = min(n, len(ids))
-        per = int(math.ceil(len(ids) / n))
-        unit = cost / len(ids)
-        for s in range(0, len(ids), per):
-            chunk = ids[s:s + per]
-            pieces.append((unit * len(chunk), chunk[0], chunk))
-    pieces.sort(key=lambda x: (-x[0], x[1]))
-    load = [0.0] * world
-    rank_of = np.empty(len(specs), dtype=np.int64)
-    for cost, _, chunk in pieces:
-        r = min(range(world), key=lambda k: (load[k], k))
-        load[r] += cost
-        rank_of[chunk] = r
+def cell_costs(specs, lengths):
+    """Modelled cost of every cell: frames x bins x algorithm weight."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    if isinstance(specs, JobSpecs):
+        nf = np.concatenate([[int(p["n_fft"]) for p in specs.cells[a]] for a in specs.algorithms])
+        hp = np.concatenate([[int(p["hop_length"]) for p in specs.cells[a]] for a in specs.algorithms])
+        wt = np.concatenate([[ALGO_WEIGHT.get(a, 1.0)] * len(specs.cells[a])
+                             for a in specs.algorithms])
+        off = np.concatenate([[0], np.cumsum([len(specs.cells[a]) for a in specs.algorithms])[:-1]])
+        g = off[specs.alg] + specs.cell
+        return (1 + lengths[specs.pair] // hp[g]) * (nf[g] // 2 + 1) * wt[g]
+    return np.array([frames(lengths[pair], p["hop_length"]) * (int(p["n_fft"]) // 2 + 1)
+                     * ALGO_WEIGHT.get(alg, 1.0) for (pair, alg, p) in specs], dtype=np.float64)
+
+
+def assign_shards(specs, lengths, world):
+    """Rank of every cell and each rank's modelled load: the job cut into
+    ``world`` contiguous runs of cell ids of equal modelled cost (a cell goes to
+    the run its cost midpoint falls in).
+
+    Cell ids run pairs -> algorithms -> grid (job_specs), so a rank holds whole
+    pairs plus at most a part of one pair at each end of its run: the per-pair
+    analysis (STFT and noise PSDs of each (n_fft, hop)) runs on at most
+    ceil(pairs / world) + 1 pairs per rank, and every rank gets the same mix of
+    algorithms and hops, so an error in the cost model (ALGO_WEIGHT) shifts
+    every rank alike.  (A greedy LPT over (pair, n_fft, hop, algorithm) items,
+    r01-r02, spread each pair's items over many ranks: at world 8 on the
+    100-pair job every rank ran the analysis of 25 pairs instead of 13.)"""
+    cost = cell_costs(specs, lengths).astype(np.float64)
+    n = len(cost)
+    rank_of = np.zeros(n, dtype=np.int64)
+    if world > 1 and n:
+        total = float(cost.sum())
+        mid = np.cumsum(cost) - 0.5 * cost
+        rank_of = np.minimum((mid * world / total).astype(np.int64), world - 1)
+    load = np.bincount(rank_of, weights=cost, minlength=world).tolist() if n else [0.0] * world
     return rank_of, load
 
 
 def engine_compute(clean, noisy, specs, ids, engine=None, align=True, stoi=True):
-    """Device compute of the cells ``ids``: per-cell (sse, snr, finite, stoi),
-    scored after finalize_enhanced's alignment (align=False: at lag 0).
-    stoi=False leaves the STOI column NaN (no waveforms are kept).
+    """Device compute of the cells ``ids``: per-cell (sse, snr, finite, stoi,
+    lag, xstatus), scored after finalize_enhanced's alignment (align=False: at
+    lag 0, lag and xstatus 0).  stoi=False leaves the STOI column NaN (no
+    waveforms are kept).
 
     clean/noisy: lists of 1-D float arrays (host) indexed by pair.  Pairs are
     batched by length (the engine's signal batches are rectangular), and, when
@@ -211,12 +230,33 @@ def engine_compute(clean, noisy, specs, ids, engine=None, align=True, stoi=True)
     job_specs' JobSpecs, cells the engine computes identically (a quarter of
     the HEAD grid: min_tracking ignores noise_percentile) are computed once
     and their rows copied, and batches of the same structure reuse one device
-    plan (Engine.run(reuse=...))."""
+    plan (Engine.run(reuse=...)).
+
+    Device memory: an engine made here is dropped with its cached plans on
+    return.  A caller's engine keeps its plan_cache_size; the STOI path holds
+    two plans while it runs (double-buffered waveforms: 2 x STOI_WAVE_BYTES =
+    64 GB peak plus each plan's analysis buffers) and trims the cache back to
+    the caller's size on return."""
+    from .engine import Engine
+    own = engine is None
+    eng = engine or Engine()
+    size0 = eng.plan_cache_size
+    try:
+        return _engine_compute(eng, clean, noisy, specs, ids, align, stoi)
+    finally:
+        if own:
+            eng._plan_cache.clear()
+        else:
+            eng.plan_cache_size = size0
+            while len(eng._plan_cache) > max(size0, 1):
+                eng._plan_cache.popitem(last=False)
+
+
+def _engine_compute(eng, clean, noisy, specs, ids, align, stoi):
     import hashlib
     import torch
-    from .engine import Engine, snr_db, spec_fingerprint
+    from .engine import snr_db, spec_fingerprint
     from .metrics import StoiPlan
-    eng = engine or Engine()
     ids = np.asarray(ids, dtype=np.int64)
     lengths = [len(x) for x in noisy]
     js_specs = isinstance(specs, JobSpecs)
@@ -318,6 +358,11 @@ def engine_compute(clean, noisy, specs, ids, engine=None, align=True, stoi=True)
             vals[js, 0] = res["sse"]
             vals[js, 1] = snr_db(res["sse"], cpow[sig])
             vals[js, 2] = res["finite"]
+            if "lag" in res:
+                vals[js, 4] = res["lag"]
+                vals[js, 5] = res["xcorr_status"]
+            else:
+                vals[js, 4:6] = 0
             del res
     for item in inflight:
         collect(item)
@@ -403,7 +448,8 @@ def select_best(specs, table, objective="snr", tol=None):
 
 def run_grid(clean, noisy, specs, compute=None, group=None, device=None, objective="snr"):
     """Run every cell of ``specs`` across the ranks of ``group`` (or locally)
-    and return (table [n_cells, NCOL] = sse, snr, finite, stoi, winners).  Every rank
+    and return (table [n_cells, NCOL] = sse, snr, finite, stoi, lag, xstatus;
+    winners).  Every rank
     gets the full table (all_gather); the selection is the deterministic
     sequential scan, identical on every rank."""
     import torch.distributed as dist
@@ -411,7 +457,7 @@ def run_grid(clean, noisy, specs, compute=None, group=None, device=None, objecti
     world = dist.get_world_size(group) if dist_on else 1
     rank = dist.get_rank(group) if dist_on else 0
     lengths = [len(x) for x in noisy]
-    rank_of, _ = assign_lpt(specs, lengths, world)
+    rank_of, _ = assign_shards(specs, lengths, world)
     ids = np.nonzero(rank_of == rank)[0]
     compute = compute or engine_compute
     vals = compute(clean, noisy, specs, ids) if len(ids) else np.zeros((0, NCOL))

@@ -268,11 +268,12 @@ int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n
  *     status[c]       CSE_XCORR_*
  *     corr            optional [n_cells][2 max_lag + 1] f32 c(l) (diagnostics), or NULL
  * Lags whose fp32 FFT correlation lies within 2e-5 ||r0|| ||s0|| of the maximum
- * are re-evaluated exactly in fp64 (at most 64; more -> AMBIGUOUS, fp32 argmax).
+ * are re-evaluated exactly in fp64, every one of them: the lag is exact in both
+ * OK and FLAT status (FLAT only reports that the slow path ran).
  */
 enum {
     CSE_XCORR_OK = 0,
-    CSE_XCORR_AMBIGUOUS = 1, /* > 64 near-maximal lags: fp32 argmax kept */
+    CSE_XCORR_FLAT = 1,      /* > 64 near-maximal lags (flat correlation), all re-evaluated in fp64 */
     CSE_XCORR_NONFINITE = 2, /* non-finite output head: no alignment */
 };
 int64_t cse_xcorr_workspace_bytes(int64_t n_sig, int64_t len, int n, int max_lag);

@@ -28,7 +28,8 @@ def pairs(n=3, seconds=0.3):
 
 
 def oracle_compute(clean, noisy, specs, ids, align=True, stoi=True):
-    """Per-cell (sse, snr, finite, stoi) from the CPU oracle: finalize_enhanced
+    """Per-cell (sse, snr, finite, stoi, lag, xstatus = 0) from the CPU oracle
+    (search.RECORD_FIELDS without cell_id): finalize_enhanced
     (alignment, length match, finiteness, clip) then calculate_snr and
     calculate_stoi, like the reference's grid loop
     (speech_enhancement_comparison.py:165-180); align=False scores the clipped
@@ -36,7 +37,7 @@ def oracle_compute(clean, noisy, specs, ids, align=True, stoi=True):
     output rounded to f32, the type the device writes."""
     import oracle
     from oracle import stoi_ref
-    out = np.zeros((len(ids), 4))
+    out = np.zeros((len(ids), 6))
     for j, cid in enumerate(ids):
         pair, alg, p = specs[cid]
         kw = dict(p)
@@ -45,15 +46,17 @@ def oracle_compute(clean, noisy, specs, ids, align=True, stoi=True):
         y = oracle.ALGORITHMS[alg](noisy[pair], 16000, **kw)
         c = np.asarray(clean[pair], np.float64)
         e = oracle.finalize_enhanced(y, c, 16000, do_align=align)
+        lag = (oracle.align_lag(c, y, 16000) or 0) if align else 0
         if e is None:
-            out[j] = (np.nan, np.nan, 0, np.nan)
+            out[j] = (np.nan, np.nan, 0, np.nan, 0, 0)
             continue
         st = None
         if stoi:
             e32 = oracle.finalize_enhanced(np.asarray(y, np.float32).astype(np.float64), c, 16000,
                                            do_align=align)
             st = stoi_ref.calculate_stoi(c, e32, 16000)
-        out[j] = (np.sum((c - e) ** 2), oracle.calculate_snr(c, e), 1, np.nan if st is None else st)
+        out[j] = (np.sum((c - e) ** 2), oracle.calculate_snr(c, e), 1,
+                  np.nan if st is None else st, lag, 0)
     return out
 
 
@@ -94,3 +97,35 @@ def oracle_cell_full(args):
     e32 = oracle.finalize_enhanced(np.asarray(y, np.float32).astype(np.float64), clean, 16000)
     st = stoi_ref.calculate_stoi(clean, e32, 16000)
     return y, int(lag), snr, np.nan if st is None else st
+
+
+_PAIR_CACHE = {}
+
+
+def oracle_cell_scores(args):
+    """(cell id, sse, snr, finite, stoi, lag) of one cell through the oracle,
+    scored like the reference's grid loop (speech_enhancement_comparison.py:
+    165-180: finalize_enhanced, calculate_snr, calculate_stoi of the output
+    rounded to f32, the type the device writes).  The pair is synthesised in
+    the worker (make_pair(pair, seconds)).  Pool worker."""
+    import oracle
+    from oracle import stoi_ref
+    from classical_speech_enhancement_amd.synth import make_pair
+    cid, pair, alg, p, seconds = args
+    key = (pair, seconds)
+    if key not in _PAIR_CACHE:
+        _PAIR_CACHE.clear()
+        _PAIR_CACHE[key] = make_pair(pair, seconds)
+    clean, noisy = _PAIR_CACHE[key]
+    kw = dict(p)
+    if kw["noise_method"] == "true_noise":
+        kw["clean_audio"] = clean
+    y = oracle.ALGORITHMS[alg](noisy, 16000, **kw)
+    e = oracle.finalize_enhanced(y, clean, 16000)
+    if e is None:
+        return cid, np.nan, np.nan, 0.0, np.nan, 0
+    lag = oracle.align_lag(clean, y, 16000) or 0
+    e32 = oracle.finalize_enhanced(np.asarray(y, np.float32).astype(np.float64), clean, 16000)
+    st = stoi_ref.calculate_stoi(clean, e32, 16000)
+    return (cid, float(np.sum((clean - e) ** 2)), oracle.calculate_snr(clean, e), 1.0,
+            np.nan if st is None else st, int(lag))

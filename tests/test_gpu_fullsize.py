@@ -10,7 +10,10 @@ once in this process (world 1) and once sharded over two gloo ranks sharing the
 card (the 8-GPU node runs the same code over RCCL).
 
 Checked: every cell finite; min_tracking cells that differ only in
-noise_percentile (which that estimator ignores) bit-identical; the table
+noise_percentile (which that estimator ignores) bit-identical (copied in the
+deduplicated sweep, computed separately in a plain-list job); the alignment
+status of every cell counted (no non-finite head; lags of the flat-correlation
+cells, if any, against the oracle); the table
 identical across shardings; 64 cells stratified over algorithm x n_fft x hop x
 noise method against the oracle: waveform rel-L2 and rel-max <= 1e-5 (the
 north-star tolerance), the alignment lag equal, the aligned SNR within
@@ -83,7 +86,7 @@ def tables(tmp_path_factory):
 
 def test_full_sweep_shape_finite_and_sharding(tables):
     t, specs = tables["table"], tables["specs"]
-    assert len(specs) == N_PAIRS * 9744 and t.shape == (len(specs), 4)
+    assert len(specs) == N_PAIRS * 9744 and t.shape == (len(specs), 6)
     assert t[:, 2].all(), "non-finite cells"
     assert np.isfinite(t[:, 1]).all()
     assert np.isfinite(t[:, 3]).all()  # 10-s clips: every cell has >= 30 STOI frames
@@ -95,7 +98,10 @@ def test_full_sweep_shape_finite_and_sharding(tables):
     assert all(c >= 0 for c, _ in search.select_best(specs, t, "stoi").values())
 
 
-def test_min_tracking_duplicates_bit_identical(tables):
+def test_min_tracking_duplicate_rows_copied(tables):
+    """The sweep computes each min_tracking duplicate (cells that differ only in
+    noise_percentile, which that estimator ignores) once and copies its row:
+    this checks the copy.  The engine-level identity is checked below."""
     t, specs = tables["table"], tables["specs"]
     first, n = {}, 0
     for cid, (pair, alg, p) in enumerate(specs):
@@ -108,6 +114,48 @@ def test_min_tracking_duplicates_bit_identical(tables):
         else:
             first[k] = cid
     assert n == N_PAIRS * 9744 // 4
+
+
+def test_min_tracking_duplicates_computed_separately_bit_identical(tables):
+    """A plain-list job (not JobSpecs, so no deduplication): every min_tracking
+    cell of 2 pairs x the full grid goes through the engine on its own, aligned
+    and STOI-scored, and each duplicate's row equals its twin's bit for bit."""
+    from classical_speech_enhancement_amd import search
+    specs = [s for s in tables["specs"][:2 * 9744] if s[2]["noise_method"] == "min_tracking"]
+    vals = search.engine_compute(tables["clean"], tables["noisy"], specs, np.arange(len(specs)))
+    first, n = {}, 0
+    for cid, (pair, alg, p) in enumerate(specs):
+        k = (pair, alg) + tuple((a, b) for a, b in p.items() if a != "noise_percentile")
+        if k in first:
+            assert np.array_equal(vals[cid], vals[first[k]], equal_nan=True), (pair, alg, p)
+            n += 1
+        else:
+            first[k] = cid
+    assert n == len(specs) // 2 == 2 * 9744 // 4
+
+
+def test_alignment_status_counted_flat_cells_exact(tables):
+    """cse_xcorr_lag's status over all 974,400 cells (search table column
+    'xstatus'): no non-finite head; FLAT cells (more than 64 near-maximal lags,
+    every one re-evaluated in fp64) are counted, and up to 32 of them are
+    checked against the oracle's lag."""
+    import multiprocessing as mp
+    from _grid_worker import oracle_cell_full
+    t, specs = tables["table"], tables["specs"]
+    st = t[:, 5].astype(np.int64)
+    lag = t[:, 4]
+    print(f"xcorr status: ok {(st == 0).sum()}, flat {(st == 1).sum()}, nonfinite "
+          f"{(st == 2).sum()}; non-zero lags {(lag != 0).sum()} of {len(t)}")
+    assert (st == 2).sum() == 0
+    flat = np.flatnonzero(st == 1)
+    if len(flat) == 0:
+        return
+    pick = flat[np.linspace(0, len(flat) - 1, min(32, len(flat))).astype(np.int64)]
+    procs = max(1, min(16, len(os.sched_getaffinity(0))))
+    with mp.get_context("spawn").Pool(procs) as pool:
+        ref = pool.map(oracle_cell_full, [specs[int(c)] + (SECONDS,) for c in pick], chunksize=1)
+    for c, (_, lag_ref, _, _) in zip(pick, ref):
+        assert int(lag[c]) == lag_ref, (int(c), lag[c], lag_ref)
 
 
 def test_stratified_cells_match_oracle(tables):

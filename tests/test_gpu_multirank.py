@@ -87,7 +87,7 @@ def test_run_grid_two_ranks_equals_one_process(gpu, tmp_path):
 
 
 def test_bench_two_ranks_strong_scaling(gpu):
-    """--pairs-total: the fixed job's cells split by search.assign_lpt; value
+    """--pairs-total: the fixed job's cells split by search.assign_shards; value
     counts the whole job once."""
     env = dict(os.environ, CSE_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
@@ -153,3 +153,36 @@ def test_run_grid_rccl_world1_equals_local(gpu, tmp_path):
     specs = search.job_specs(len(noisy), grids=SMALL_GRIDS)
     ref, _ = search.run_grid(clean, noisy, specs)
     assert np.array_equal(t0, ref, equal_nan=True)
+
+
+def test_bench_eight_ranks_strong_scaling_rehearsal(gpu, tmp_path):
+    """The 8-GPU node's strong-scaling run, rehearsed with 8 gloo ranks sharing
+    the card: BASELINE config 4's 100-pair job sharded by search.assign_shards.
+    The line counts the whole job once, each rank holds at most 14 pairs (whole
+    pairs plus a part at each end of its run), and the gathered per-cell
+    records equal a world-1 run's bit for bit."""
+    common = ["--steps", "1", "--warmup", "1", "--pairs-total", "100", "--full-grid-steps", "0",
+              "--no-sweep", "--no-cpu-baseline", "--no-parity"]
+    env = dict(os.environ, CSE_DIST_BACKEND="gloo")
+    t8, t1 = tmp_path / "t8.npy", tmp_path / "t1.npy"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "8", "--dump-table", str(t8)] + common
+    out = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=420)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert d["n_gpus"] == 8 and d["scaling"] == "strong"
+    assert d["config"]["units_per_step"] == 100 * 4572372
+    assert d["config"]["cells_total"] == d["config"]["gathered_cells_finite"] == 487200
+    assert d["config"]["pairs_rank0"] <= 14
+    assert abs(d["config"]["units_per_step_rank0"] - 100 * 4572372 / 8) < 0.02 * 100 * 4572372 / 8
+    assert d["value"] == pytest.approx(d["config"]["units_per_step"] / (d["ms_per_step"] / 1e3),
+                                       rel=1e-6)
+    one = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--dump-table", str(t1)]
+                         + common, cwd=REPO, capture_output=True, text=True, timeout=420)
+    assert one.returncode == 0, one.stderr[-3000:]
+    a, b = np.load(t8), np.load(t1)
+    assert a.shape == b.shape == (487200, 2)
+    assert np.array_equal(a, b)
+    print("8-rank rehearsal:", d["config"]["parallelism"], "pairs on rank 0:",
+          d["config"]["pairs_rank0"], "ms/step", d["ms_per_step"])

@@ -1,0 +1,119 @@
+"""Winner-index parity at config scale (needs a GPU).
+
+The reference's product is the cell its sequential best-so-far scan selects
+per (pair, algorithm) (speech_enhancement_comparison.py:186-216), after every
+cell was aligned by an argmax over lags (:60) and scored.  Both are index
+work, so this test runs complete 10-s grids through the device sweep
+(search.run_grid: STFT, noise PSDs, fused enhance, alignment, SNR, STOI) and
+through the oracle (a CPU pool, the reference's algorithm per cell), then
+compares, cell by cell and group by group:
+
+  - the alignment lag of every cell: equal;
+  - SNR within 2e-4 dB and STOI within 2e-6 of the oracle's, every cell;
+  - the scan's winner id for both device objectives (SNR, STOI).  A winner may
+    differ only on a near-tie: the scan's final score lies in [max - tol, max]
+    for any score vector, so with per-cell score errors <= err the two winners'
+    oracle scores differ by at most tol + 2 err.  Mismatches are counted and
+    their gaps printed, and each must satisfy that bound.
+
+Cells: pairs 0-3 with the whole spectral-subtraction (720) and Wiener (192)
+grids, pair 0 with the whole MMSE grid (1,920), and pair 0's OMLSA grid every
+8th cell (864; the scan runs over that sub-list in grid order, which is the
+same scan on fewer cells).  6,432 10-s cells in 10 (pair, algorithm) groups.
+"""
+
+import os
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SECONDS = 10.0
+N_PAIRS = 4
+SNR_ERR = 2e-4
+STOI_ERR = 2e-6
+
+
+@pytest.fixture(scope="module")
+def tables():
+    import multiprocessing as mp
+    import torch
+    if torch.cuda.device_count() == 0:
+        pytest.skip("no GPU")
+    from classical_speech_enhancement_amd import search
+    from classical_speech_enhancement_amd.synth import make_pair
+    from _grid_worker import oracle_cell_scores
+    pairs = [make_pair(i, SECONDS) for i in range(N_PAIRS)]
+    clean = [c for c, _ in pairs]
+    noisy = [x for _, x in pairs]
+    specs = search.job_specs(N_PAIRS)
+    t0 = time.perf_counter()
+    table, _ = search.run_grid(clean, noisy, specs)
+    print(f"device sweep of {len(specs)} cells: {time.perf_counter() - t0:.2f} s", flush=True)
+    chosen = []
+    for cid in range(len(specs)):
+        pair, alg = int(specs.pair[cid]), specs.algorithms[int(specs.alg[cid])]
+        c = int(specs.cell[cid])
+        if alg in ("spectralSubtractor", "wiener") or (pair == 0 and alg == "mmse") or \
+                (pair == 0 and alg == "omlsa" and c % 8 == 0):
+            chosen.append(cid)
+    chosen = np.asarray(chosen, dtype=np.int64)
+    work = [(int(c),) + tuple(specs[int(c)]) + (SECONDS,) for c in chosen]
+    procs = max(1, min(16, len(os.sched_getaffinity(0))))
+    ref = np.full((len(specs), 5), np.nan)
+    t0 = time.perf_counter()
+    with mp.get_context("spawn").Pool(procs) as pool:
+        for k, (cid, sse, snr, fin, st, lag) in enumerate(
+                pool.imap_unordered(oracle_cell_scores, work, chunksize=4)):
+            ref[cid] = (sse, snr, fin, st, lag)
+            if (k + 1) % 500 == 0:
+                print(f"oracle: {k + 1}/{len(work)} cells, {time.perf_counter() - t0:.0f} s",
+                      flush=True)
+    return dict(specs=specs, table=table, ref=ref, chosen=chosen)
+
+
+def test_every_cell_lag_and_scores(tables):
+    t, ref, ids = tables["table"], tables["ref"], tables["chosen"]
+    assert np.array_equal(t[ids, 2], ref[ids, 2]), "finiteness differs"
+    assert (t[ids, 2] == 1).all()
+    st = t[ids, 5].astype(np.int64)
+    print(f"xcorr status over {len(ids)} cells: ok {(st == 0).sum()}, flat {(st == 1).sum()}, "
+          f"nonfinite {(st == 2).sum()}; non-zero lags {(t[ids, 4] != 0).sum()}")
+    bad = np.flatnonzero(t[ids, 4] != ref[ids, 4])
+    assert len(bad) == 0, [(int(ids[b]), t[ids[b], 4], ref[ids[b], 4]) for b in bad[:10]]
+    dsnr = np.abs(t[ids, 1] - ref[ids, 1])
+    dstoi = np.abs(t[ids, 3] - ref[ids, 3])
+    print(f"max |SNR - oracle| {dsnr.max():.3e} dB, max |STOI - oracle| {dstoi.max():.3e}")
+    assert dsnr.max() <= SNR_ERR
+    assert dstoi.max() <= STOI_ERR
+
+
+@pytest.mark.parametrize("objective,col,err", [("snr", 1, SNR_ERR), ("stoi", 3, STOI_ERR)])
+def test_winner_ids(tables, objective, col, err):
+    from classical_speech_enhancement_amd import search
+    specs, t, ref, ids = tables["specs"], tables["table"], tables["ref"], tables["chosen"]
+    sub = [specs[int(c)] for c in ids]
+    tdev = t[ids][:, :4]
+    tref = ref[ids][:, :4]
+    tol = search.TOLERANCE[objective]
+    dev_best = search.select_best(sub, tdev, objective)
+    ref_best = search.select_best(sub, tref, objective)
+    assert dev_best.keys() == ref_best.keys()
+    mism, gaps = 0, []
+    for key in dev_best:
+        d, _ = dev_best[key]
+        r, _ = ref_best[key]
+        assert d >= 0 and r >= 0, key
+        if d == r:
+            continue
+        mism += 1
+        members = [j for j, s in enumerate(sub) if (s[0], s[1]) == key]
+        e = float(np.max(np.abs(tdev[members, col] - tref[members, col])))
+        gap = abs(tref[d, col] - tref[r, col])
+        gaps.append((key, int(ids[d]), int(ids[r]), gap, e))
+        assert tref[d, col] >= tref[r, col] - (tol + 2 * e), gaps[-1]
+        assert tdev[r, col] >= tdev[d, col] - (tol + 2 * e), gaps[-1]
+    print(f"{objective}: {len(dev_best)} (pair, algorithm) groups, {mism} winner ids differ "
+          f"(near-ties within tol {tol:g} + 2 x score error): {gaps}")

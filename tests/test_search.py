@@ -1,4 +1,4 @@
-"""Grid-search driver: enumeration order, LPT sharding, the records gather
+"""Grid-search driver: enumeration order, contiguous cost-balanced sharding, the records gather
 over world_size 2 and 4 (gloo, CPU) and the reference's sequential selection
 (speech_enhancement_comparison.py:149-216)."""
 
@@ -27,22 +27,43 @@ def test_job_specs_follow_reference_order():
 
 
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
-def test_lpt_assigns_every_cell_and_balances(world):
+def test_shards_assign_every_cell_and_balance(world):
     specs = search.job_specs(3, n_fft=512)
     lengths = [160000] * 3
-    rank_of, load = search.assign_lpt(specs, lengths, world)
+    rank_of, load = search.assign_shards(specs, lengths, world)
     assert rank_of.min() >= 0 and rank_of.max() < world
     assert len(set(rank_of.tolist())) == world
     assert max(load) <= 1.15 * (sum(load) / world)
-    again, _ = search.assign_lpt(specs, lengths, world)
+    again, _ = search.assign_shards(specs, lengths, world)
     assert np.array_equal(rank_of, again)
 
 
-def test_lpt_keeps_group_cells_together_when_possible():
+def test_shards_keep_group_cells_together_when_possible():
     specs = search.job_specs(16, n_fft=512)
-    rank_of, _ = search.assign_lpt(specs, [160000] * 16, 2)
+    rank_of, _ = search.assign_shards(specs, [160000] * 16, 2)
     for key, ids in _groups(specs).items():
         assert len(set(rank_of[ids].tolist())) == 1, key
+
+
+def test_shards_are_pair_affine_at_world_8():
+    """The bench's 100-pair job at world 8: every rank runs the analysis of at
+    most ceil(100/8) + 1 = 14 pairs (28 (pair, hop) groups at n_fft 512, was 50
+    with the r02 LPT), modelled loads within 1.02 of each other, and the
+    JobSpecs and plain-list cost paths agree."""
+    specs = search.job_specs(100, n_fft=512)
+    lengths = [160000] * 100
+    rank_of, load = search.assign_shards(specs, lengths, 8)
+    assert max(load) <= 1.02 * min(load)
+    for r in range(8):
+        ids = np.flatnonzero(rank_of == r)
+        assert (np.diff(ids) == 1).all()  # one contiguous run
+        pairs = set(specs.pair[ids].tolist())
+        hops = {(int(specs.pair[c]), specs[int(c)][2]["hop_length"]) for c in ids}
+        assert len(pairs) <= 14 and len(hops) <= 28, (r, len(pairs), len(hops))
+    small = search.job_specs(3, grids=SMALL_GRIDS)
+    a, la = search.assign_shards(small, [4000, 9000, 4000], 4)
+    b, lb = search.assign_shards(list(small), [4000, 9000, 4000], 4)
+    assert np.array_equal(a, b) and np.allclose(la, lb)
 
 
 def _groups(specs):

@@ -76,6 +76,9 @@ def derive(pmc, kernel_ms):
 
 
 def main(tag, rnd, units512=None, units1024=None):
+    sys.path.insert(0, REPO)
+    import bench
+    src_sha = bench.kernel_src_sha()  # the sources the profiled .so was built from
     base = os.path.join(REPO, "gpurun_out", f"prof_{tag}")
     kt = {}
     for name in ("512", "1024", "sweep"):
@@ -113,6 +116,10 @@ def main(tag, rnd, units512=None, units1024=None):
                "grbm_gui_active": pmc.get("GRBM_GUI_ACTIVE"),
                "sq_busy_cycles": pmc.get("SQ_BUSY_CYCLES"),
                "valu_frac": k.get("valu_frac"), "clock_ghz_profiled": k.get("clock_ghz_profiled"),
+               "valu_issue_cycles": k.get("valu_issue_cycles"),
+               "share_wait_inst_any": k.get("share_wait_inst_any"),
+               "lds_conflict_cycles_per_lds_inst": k.get("lds_conflict_cycles_per_lds_inst"),
+               "kernel_src_sha": src_sha,
                "source": f"profiles/{rnd}_kernels.json (tools/profile_all.sh {tag})"}
         json.dump(out, open(os.path.join(REPO, "profiles", f"pmc_{key}_{rnd}.json"), "w"), indent=1)
     for key, k in summary["kernels"].items():
