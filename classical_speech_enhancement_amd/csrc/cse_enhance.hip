@@ -25,6 +25,13 @@
 #include "cse_common.hpp"
 #include "cse_special.hpp"
 
+#ifndef CSE_JIT_TABLES
+#define CSE_JIT_TABLES 0  // experiment: table reads just before use (register pressure)
+#endif
+#ifndef CSE_ROT_TABLE_1024
+#define CSE_ROT_TABLE_1024 0  // 1024: packing rotors as base x W32^j (the table measured slower)
+#endif
+
 namespace cse {
 
 template <int NFFT>
@@ -93,25 +100,29 @@ __device__ __forceinline__ float mmse_bracket(float v, float sqrtv) {
 // prev_gain**2 * prev_gamma (wiener_filter.py:133, mmse.py:82,
 // advanced_mmse.py:215): the carried state is rr = (G*G)*gamma.
 // ---------------------------------------------------------------------------
+// d = max(gamma - 1, 0) (the ML estimate of the DD rule) is per bin too: the
+// n_fft = 512 stager stores the row (gamma, d) (cells compute d themselves at
+// 1024, whose rows do not fit the LDS budget twice as wide).
 // First frame: the reference uses xi = d (Wiener) / max(gamma-1, ksi_min)
 // (MMSE, OMLSA); with rr = 0 and alpha_t = 0 on frame 0 the general DD
-// expression alpha_t*rr + (1-alpha_t)*max(gamma-1, 0) gives exactly that (for
-// ksi_min >= 0), so there is no per-bin branch to split the scheduling region.
-__device__ __forceinline__ float gain_wiener(float gam, float& rr, float alpha_t, float gfloor) {
-    const float d = fmaxf(gam - 1.0f, 0.0f);
+// expression alpha_t*rr + (1-alpha_t)*d gives exactly that (for ksi_min >= 0),
+// so there is no per-bin branch to split the scheduling region.
+__device__ __forceinline__ float gain_wiener(float gam, float d, float& rr, float alpha_t,
+                                             float gfloor) {
     const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * d, 1e-10f);
     const float g = fminf(fmaxf(xi * fast_rcp(1.0f + xi), gfloor), 1.0f);
     rr = (g * g) * gam;
     return g;
 }
 
-__device__ __forceinline__ float gain_mmse(float gam, float& rr, float alpha_t, float ksi_min,
-                                           float gmin, float gmax) {
-    const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * fmaxf(gam - 1.0f, 0.0f), ksi_min);
+// cig = (sqrt(pi)/2) / (gamma + 1e-12), per bin from the row stager
+__device__ __forceinline__ float gain_mmse(float gam, float d, float cig, float& rr, float alpha_t,
+                                           float ksi_min, float gmin, float gmax) {
+    const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * d, ksi_min);
     const float v = __builtin_amdgcn_fmed3f(xi * gam * fast_rcp(1.0f + xi), 1e-12f, 80.0f);
     const float sv = __builtin_amdgcn_sqrtf(v);
     const float h = mmse_bracket(v, sv);
-    float g = (0.88622692545275801f * (sv * fast_rcp(gam + 1e-12f))) * h;
+    float g = (sv * cig) * h;
     // nan_to_num(nan -> gmin, +inf -> gmax, -inf -> gmin) + clip (mmse.py:98-104):
     // fmaxf returns the non-NaN operand, so the clip alone does all of it.
     g = fminf(fmaxf(g, gmin), gmax);
@@ -130,9 +141,10 @@ __device__ __forceinline__ float gain_mmse(float gam, float& rr, float alpha_t, 
 // 0 <= X <= 1e6, so lg is finite or -inf (xi = 0 with ksi_min = 0), and -inf
 // gives g = exp2(-inf) = 0 -> clip -> gain_floor, the reference's 0**p * gf**(1-p)
 // clipped (p >= 1e-10 > 0).  Non-finite input makes the cell non-finite either way.
-__device__ __forceinline__ float gain_omlsa(float gam, float& rr, float alpha_t, float ksi_min,
-                                            float gfloor, float lg2_floor, float q, float vmax) {
-    const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * fmaxf(gam - 1.0f, 0.0f), ksi_min);
+__device__ __forceinline__ float gain_omlsa(float gam, float d, float& rr, float alpha_t,
+                                            float ksi_min, float gfloor, float lg2_floor, float q,
+                                            float vmax) {
+    const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * d, ksi_min);
     const float r = fast_rcp(1.0f + xi);
     const float xr = xi * r;
     const float v = __builtin_amdgcn_fmed3f(xr * gam, 1e-12f, vmax);
@@ -141,7 +153,9 @@ __device__ __forceinline__ float gain_omlsa(float gam, float& rr, float alpha_t,
     const float lg = fast_log2(xr * __builtin_amdgcn_rsqf(vc)) + Q;
     const float ev = fast_exp2(v * kLog2e);
     const float A = q * (r * ev) + 1e-10f;
-    const float p = fminf(fmaxf(A * fast_rcp(A + (1.0f - q)), 0.0f), 1.0f);
+    // A >= 1e-10 and 1 - q > 0: p lies in (0, 1) up to one rounding, so the
+    // reference's clip (advanced_mmse.py:116) needs no instruction
+    const float p = A * fast_rcp(A + (1.0f - q));
     const float g = fast_exp2(lg2_floor + p * (lg - lg2_floor));
     const float G = __builtin_amdgcn_fmed3f(g, gfloor, 1.0f);  // g >= 0, never NaN
     rr = (G * G) * gam;
@@ -192,11 +206,17 @@ struct WG {
     static constexpr int CREG_RAW = XB > TB ? XB : TB;
     static constexpr int CREG_U = (CREG_RAW + 127) / 128;
     static constexpr int CREG = (CREG_U + (CREG_U % 2 ? 0 : 1)) * 128;
+    // shared rows (double-buffered): Y (float2 [B]); G (float [B], or the
+    // (gamma, d) / (N, P) float2 [B] at 512); A (float [B], 512: MMSE's
+    // c/(gamma + 1e-12), SS's 1/|Y|); clean (float [HMAX])
+    static constexpr bool R2 = (NFFT == 512);
     static constexpr int YROW = ((G::B * 8 + 15) / 16) * 16;      // bytes of one Y row
-    static constexpr int GROW = ((G::B * 4 + 15) / 16) * 16;      // bytes of one gamma / N row
+    static constexpr int GROW = ((G::B * (R2 ? 8 : 4) + 15) / 16) * 16;
+    static constexpr int AROW = R2 ? ((G::B * 4 + 15) / 16) * 16 : 0;
     static constexpr int OFF_Y = CPWG * CREG;                     // float2[2][B] (double buffer)
-    static constexpr int OFF_G = OFF_Y + 2 * YROW;                // float[2][B]
-    static constexpr int OFF_C = OFF_G + 2 * GROW;                // float[2][HMAX]
+    static constexpr int OFF_G = OFF_Y + 2 * YROW;
+    static constexpr int OFF_A = OFF_G + 2 * GROW;
+    static constexpr int OFF_C = OFF_A + 2 * AROW;                // float[2][HMAX]
     static constexpr int CBUF = 2 * HMAX * 4;
     // n_fft 1024 keeps two tables small.  The window keeps slots q < 16, since
     // slot q + 16 is n + N/2 and w(n + N/2) = 1 - w(n) (the full 32-slot table
@@ -214,18 +234,21 @@ struct WG {
     // b - 1: the ds_read_b128 of a 16-lane group hit disjoint banks;
     // (1024): cf[L][2] rotors
     static constexpr int OFF_TW = OFF_C + CBUF;
-    static constexpr int OFF_LC = OFF_TW + (ROTOR_TW ? G::L * 16 : TWL * 144);  // cf[L] packing rotor
-    static constexpr int OFF_CP = OFF_LC + G::L * 8;              // float[CPWG][8]
-    // synthesis window w(n)/NFFT at the lane's 32 (16) sample slots; row stride
-    // 36 (20) floats: the lanes of a ds_read_b128 group hit disjoint banks
+    // packing rotors e^{2πi (i + L j)/NFFT}: a row of the 8 (j < 8) per lane,
+    // stride 80 B (20 dwords: the ds_read_b128 of a 16-lane group hit
+    // disjoint banks), 4 ds_read_b128 per frame instead of 7 complex products
+    static constexpr bool ROT_TABLE = R2 || CSE_ROT_TABLE_1024;
+    static constexpr int ROTSTR = 80;
+    static constexpr int OFF_LC = OFF_TW + (ROTOR_TW ? G::L * 16 : TWL * 144);
+    static constexpr int OFF_CP = OFF_LC + G::L * (ROT_TABLE ? ROTSTR : 8);  // CellParam[CPWG]
+    // synthesis window w(n)/(NFFT wss(n)) at the lane's 32 (16) sample slots,
+    // wss the steady-state window-square sum of this workgroup's hop (librosa's
+    // istft normalisation folded into the overlap-add); row stride 36 (20)
+    // floats: the lanes of a ds_read_b128 group hit disjoint banks
     static constexpr int WSLOTS = HALF_TABLES ? 16 : 32;
     static constexpr int WSTR = HALF_TABLES ? 20 : 36;
     static constexpr int OFF_WIN = OFF_CP + CPWG * 32;
-    // 1/wss at the lane's 16 retired slots, only for the one R = 2 case
-    // (512/256), whose wss is not constant; row stride 20 floats (disjoint banks)
-    static constexpr int ISTR = 20;
-    static constexpr int OFF_IWS = OFF_WIN + G::L * WSTR * 4;
-    static constexpr int BYTES = OFF_IWS + (NFFT == 512 ? G::L * ISTR * 4 : 0);
+    static constexpr int BYTES = OFF_WIN + G::L * WSTR * 4;
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
@@ -237,6 +260,7 @@ static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
               WG<1024>::CPWG == CSE_CELLS_PER_GROUP(1024), "cse.h slot-group size");
 
 // waves per SIMD the register allocation targets (VGPR budget 512 / w)
+
 #ifndef CSE_WAVES_PER_SIMD
 #define CSE_WAVES_PER_SIMD 3
 #endif
@@ -256,10 +280,20 @@ struct CellParam {
 };
 static_assert(sizeof(CellParam) == 32, "CellParam layout");
 
-// One bin: gv is gamma (Wiener/MMSE/OMLSA) or the noise PSD N (SS).
-template <int ALGO>
-__device__ __forceinline__ cf gain_bin(float2 y, float gv, float& rr, float alpha_t,
+// One bin's shared row values (staged once per workgroup and frame):
+//   Wiener/MMSE/OMLSA: g = gamma, d = max(gamma - 1, 0) (512; 1024 computes d
+//     here), a = (sqrt(pi)/2)/(gamma + 1e-12) (MMSE at 512);
+//   SS at 512: g = N, d = P = |Y|^2, a = 1/|Y| (gain output only), and the Y
+//     row holds the unit phasor of Y instead of Y ((1, 0) where Y = 0);
+//   SS at 1024: g = N with Y itself.
+struct RowV {
+    float g, d, a;
+};
+
+template <int NFFT, int ALGO>
+__device__ __forceinline__ cf gain_bin(float2 y, RowV rv, float& rr, float alpha_t,
                                        const CellParam& cp, float& g) {
+    constexpr bool R2 = (NFFT == 512);
     if (ALGO == CSE_ALGO_SS) {
         // Ps = max(P - a N, b N); |S| = sqrt(Ps) with the noisy phase
         // (spectral_subtractor.py:44-53).  No eps floor: the reference floors
@@ -267,12 +301,17 @@ __device__ __forceinline__ cf gain_bin(float2 y, float gv, float& rr, float alph
         // The raw v_sqrt/v_rsq treat denormal inputs as 0, and a near-silent
         // clip (fix_length zero-pads N, so Ps = P) reaches them: sqrt is
         // taken of a rescaled Ps below 2^-96, and the noisy phase y/|y| of a
-        // rescaled y below 2^-50.
-        const float P = y.x * y.x + y.y * y.y;
-        const float ps = fmaxf(P - cp.p0 * gv, cp.p1 * gv);
+        // rescaled y below 2^-50 (by the stager at 512).
+        const float N = rv.g;
+        const float P = R2 ? rv.d : y.x * y.x + y.y * y.y;
+        const float ps = fmaxf(P - cp.p0 * N, cp.p1 * N);
         const bool tiny_ps = ps < 0x1p-96f;
         const float sp = __builtin_amdgcn_sqrtf(tiny_ps ? ps * 0x1p64f : ps) *
                          (tiny_ps ? 0x1p-32f : 1.0f);
+        if (R2) {  // y is the phasor
+            g = sp * rv.a;
+            return cmk(sp * y.x, sp * y.y);
+        }
         const float sc = fmaxf(fabsf(y.x), fabsf(y.y)) < 0x1p-50f ? 0x1p64f : 1.0f;
         const float yx = y.x * sc, yy = y.y * sc;
         const float pz = fmaf(yx, yx, yy * yy);
@@ -280,12 +319,15 @@ __device__ __forceinline__ cf gain_bin(float2 y, float gv, float& rr, float alph
         g = (pz > 0.0f) ? u * sc : 0.0f;
         return (pz > 0.0f) ? cmk(yx * u, yy * u) : cmk(sp, 0.0f);  // angle(0) = 0
     }
-    if (ALGO == CSE_ALGO_WIENER)
-        g = gain_wiener(gv, rr, alpha_t, cp.p1);
-    else if (ALGO == CSE_ALGO_MMSE)
-        g = gain_mmse(gv, rr, alpha_t, cp.p1, cp.p2, cp.p3);
-    else
-        g = gain_omlsa(gv, rr, alpha_t, cp.p1, cp.p2, cp.lg2_floor, cp.q_spp, cp.p4);
+    const float d = R2 ? rv.d : fmaxf(rv.g - 1.0f, 0.0f);
+    if (ALGO == CSE_ALGO_WIENER) {
+        g = gain_wiener(rv.g, d, rr, alpha_t, cp.p1);
+    } else if (ALGO == CSE_ALGO_MMSE) {
+        const float cig = R2 ? rv.a : 0.88622692545275801f * fast_rcp(rv.g + 1e-12f);
+        g = gain_mmse(rv.g, d, cig, rr, alpha_t, cp.p1, cp.p2, cp.p3);
+    } else {
+        g = gain_omlsa(rv.g, d, rr, alpha_t, cp.p1, cp.p2, cp.lg2_floor, cp.q_spp, cp.p4);
+    }
     return cmk(y.x * g, y.y * g);
 }
 
@@ -303,41 +345,80 @@ __device__ __forceinline__ cf gain_bin(float2 y, float gv, float& rr, float alph
 // goes to lane (L - i) mod L through a 9-entry LDS slot per lane.  Lane 0
 // keeps the DC/Nyquist pair (Im ignored, as irfft does) and bin M/2, whose
 // Z' = 2 conj(X_{M/2}).
-// The Y / gamma row pointers are __restrict__, so the scheduler may issue the
-// bins' reads up front and interleave the independent gain chains.
+// Rows: yrow (float2 [B]), grow (float [B], or float2 [B] at 512) and arow
+// (float [B], 512: MMSE, and SS when the gain is written) of this frame.  They
+// are __restrict__, so the scheduler may issue the bins' reads up front and
+// interleave the independent gain chains.  The packing rotors e^{2πi (i + L j)/NFFT}
+// come from the lane's LDS row (8 complex).
 template <int NFFT, int ALGO, bool OUT>
-__device__ __forceinline__ void gain_pack(const float2* __restrict__ ylo, const float* __restrict__ glo,
-                                          const float2* __restrict__ yhi, const float* __restrict__ ghi,
-                                          const float2* __restrict__ ymid, const float* __restrict__ gmid,
-                                          cf (&z)[16], cf* __restrict__ xw, float (&rr)[17],
-                                          float alpha_t, const CellParam& cpar, cf base,
-                                          float* __restrict__ grow, int i) {
+__device__ __forceinline__ void gain_pack(const float2* __restrict__ yrow,
+                                          const void* __restrict__ growv,
+                                          const float* __restrict__ arow, cf (&z)[16],
+                                          cf* __restrict__ xw, float (&rr)[17], float alpha_t,
+                                          const CellParam& cpar, const float4* __restrict__ rot4,
+                                          const cf* __restrict__ base_p, float* __restrict__ gout_row,
+                                          int i) {
     constexpr int L = Geo<NFFT>::L, M = Geo<NFFT>::M;
-    // yhi / ghi point at bin M - i - 7L: bin M - i - L j is index L (7 - j).
-    // The next pair's four reads are issued before this pair's gains; the
+    constexpr bool R2 = (NFFT == 512);
+    constexpr bool WANT_A = R2 && (ALGO == CSE_ALGO_MMSE || (ALGO == CSE_ALGO_SS && OUT));
+    // per-lane bases (lo: bin i, hi: bin M - i - 7L) so that every bin's
+    // address is base + a compile-time immediate
+    const float2* ylo = yrow + i;
+    const float2* yhi = yrow + (M - i - 7 * L);
+    const float* alo = arow + i;
+    const float* ahi = arow + (M - i - 7 * L);
+    const float2* g2lo = (const float2*)growv + i;
+    const float2* g2hi = (const float2*)growv + (M - i - 7 * L);
+    const float* g1lo = (const float*)growv + i;
+    const float* g1hi = (const float*)growv + (M - i - 7 * L);
+    // hi: bin M - i - L j is index L (7 - j) from its base; M/2 is index M/2 - i
+    // from the lo base
+    auto ld = [&](bool hi, int k, float2& y, RowV& rv) {
+        y = hi ? yhi[k] : ylo[k];
+        if constexpr (R2) {
+            const float2 g2 = hi ? g2hi[k] : g2lo[k];
+            rv.g = g2.x;
+            rv.d = g2.y;
+        } else {
+            rv.g = hi ? g1hi[k] : g1lo[k];
+            rv.d = 0.0f;
+        }
+        rv.a = WANT_A ? (hi ? ahi[k] : alo[k]) : 0.0f;
+    };
+    // lane i: bins k = i + L j (lo) and M - i - L j (hi), j < 8, then M/2.
+    // The next pair's reads are issued before this pair's gains; the
     // scheduler may interleave neighbouring pairs' chains (a memory fence per
     // pair, which kept it from doing so, measured 0.3 % slower at 3 waves/SIMD).
-    float2 ya = ylo[0], yb = yhi[L * 7];
-    float ga = glo[0], gb = ghi[L * 7];
+    float2 ya, yb;
+    RowV ga, gb;
+    ld(false, 0, ya, ga);
+    ld(true, 7 * L, yb, gb);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         float2 yan, ybn;
-        float gan, gbn;
+        RowV gan, gbn;
         if (j < 7) {
-            yan = ylo[L * (j + 1)];
-            gan = glo[L * (j + 1)];
-            ybn = yhi[L * (6 - j)];
-            gbn = ghi[L * (6 - j)];
+            ld(false, L * (j + 1), yan, gan);
+            ld(true, L * (6 - j), ybn, gbn);
         } else {
-            yan = ymid[0];
-            gan = gmid[0];
+            // bin M/2 (the same for every lane): base - i + M/2
+            yan = yrow[M / 2];
+            if constexpr (R2) {
+                const float2 g2 = ((const float2*)growv)[M / 2];
+                gan.g = g2.x;
+                gan.d = g2.y;
+            } else {
+                gan.g = ((const float*)growv)[M / 2];
+                gan.d = 0.0f;
+            }
+            gan.a = WANT_A ? arow[M / 2] : 0.0f;
         }
         float g0, g1;
-        cf A = gain_bin<ALGO>(ya, ga, rr[j], alpha_t, cpar, g0);
-        cf Bm = gain_bin<ALGO>(yb, gb, rr[8 + j], alpha_t, cpar, g1);
-        if (OUT && grow) {
-            grow[i + L * j] = g0;
-            grow[M - i - L * j] = g1;
+        cf A = gain_bin<NFFT, ALGO>(ya, ga, rr[j], alpha_t, cpar, g0);
+        cf Bm = gain_bin<NFFT, ALGO>(yb, gb, rr[8 + j], alpha_t, cpar, g1);
+        if (OUT && gout_row) {
+            gout_row[i + L * j] = g0;
+            gout_row[M - i - L * j] = g1;
         }
         if (j == 0 && i == 0) {  // irfft ignores Im of DC and Nyquist
             A.y = 0.0f;
@@ -345,8 +426,15 @@ __device__ __forceinline__ void gain_pack(const float2* __restrict__ ylo, const 
         }
         const float sx = A.x + Bm.x, sy = A.y - Bm.y;
         const float dx = A.x - Bm.x, dy = A.y + Bm.y;
-        // packing rotor e^{2πi (i + L j)/NFFT} = base * W32^j
-        const cf w = (j == 0) ? base : cmul(base, cmk(Rot32::c[j], Rot32::s[j]));
+        // packing rotor e^{2πi (i + L j)/NFFT}: the lane's table row, or base * W32^j
+        cf w;
+        if constexpr (WG<NFFT>::ROT_TABLE) {
+            const float4 q4 = rot4[j >> 1];  // ds_read_b128: two rotors
+            w = (j & 1) ? cmk(q4.z, q4.w) : cmk(q4.x, q4.y);
+        } else {
+            const cf base = *base_p;
+            w = (j == 0) ? base : cmul(base, cmk(Rot32::c[j], Rot32::s[j]));
+        }
         const float px = fmaf(dx, w.x, -dy * w.y), py = fmaf(dx, w.y, dy * w.x);
         z[j] = cmk(sx - py, sy + px);
         xw[j] = cmk(sx + py, px - sy);  // Z'[M - k] for the mirror lane
@@ -358,8 +446,8 @@ __device__ __forceinline__ void gain_pack(const float2* __restrict__ ylo, const 
         }
     }
     float gm;
-    const cf Sm = gain_bin<ALGO>(ya, ga, rr[16], alpha_t, cpar, gm);
-    if (OUT && grow && i == 0) grow[M / 2] = gm;
+    const cf Sm = gain_bin<NFFT, ALGO>(ya, ga, rr[16], alpha_t, cpar, gm);
+    if (OUT && gout_row && i == 0) gout_row[M / 2] = gm;
     xw[8] = cmk(2.0f * Sm.x, -2.0f * Sm.y);
 }
 
@@ -423,22 +511,27 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             ((cf*)(smem + W::OFF_TW))[ii * 18 + b - 1] = cmk((float)c, (float)s);
         }
     }
-    // lane tables: packing rotor e^{2πi ii/NFFT}; window w(n)/NFFT at the lane's sample slots q
-    // (n = SP*(q>>1) + off + (q&1)); for 512/256 the reciprocal closed-form wss
-    // 0.75 + 0.25 cos(2π n/256) at its retired slots
+    // lane tables: packing rotors e^{2πi (ii + L j)/NFFT} (512: j < 8; 1024: j = 0);
+    // window w(n)/(NFFT S(n)) at the lane's sample slots q (n = SP*(q>>1) + off +
+    // (q&1)), S(n) = sum over m = n mod HOP + r HOP < NFFT of w(m)^2, the
+    // steady-state window-square sum librosa's istft divides by (1.5 for
+    // R = 4, 3 for R = 8, 0.75 + 0.25 cos(2π n/256) for 512/256)
     for (int e = tid; e < L * 32; e += W::THREADS) {
         const int ii = e / 32, q = e % 32;
         const int bb = (L == 16) ? ii : (ii & 15), hh = (L == 16) ? 0 : (ii >> 4);
         const int n = SP * (q >> 1) + 2 * bb + 32 * hh + (q & 1);
         const double w = 0.5 - 0.5 * cospi(2.0 * (double)n / (double)NFFT);
-        if (q < W::WSLOTS) ((float*)(smem + W::OFF_WIN))[ii * W::WSTR + q] = (float)(w / NFFT);
-        if (NFFT == 512 && HOP == 256 && q < 16)
-            ((float*)(smem + W::OFF_IWS))[ii * W::ISTR + q] =
-                (float)(1.0 / (0.75 + 0.25 * cospi(2.0 * (double)n / 256.0)));
-        if (q == 0) {
+        double S = 0.0;
+        for (int m = n % HOP; m < NFFT; m += HOP) {
+            const double wm = 0.5 - 0.5 * cospi(2.0 * (double)m / (double)NFFT);
+            S += wm * wm;
+        }
+        if (q < W::WSLOTS) ((float*)(smem + W::OFF_WIN))[ii * W::WSTR + q] = (float)(w / (NFFT * S));
+        if (W::ROT_TABLE ? q < 8 : q == 0) {
             double sn, cn;
-            sincospi(2.0 * (double)ii / (double)NFFT, &sn, &cn);
-            ((cf*)(smem + W::OFF_LC))[ii] = cmk((float)cn, (float)sn);
+            sincospi(2.0 * (double)(ii + L * q) / (double)NFFT, &sn, &cn);
+            ((cf*)(smem + W::OFF_LC + (W::ROT_TABLE ? W::ROTSTR : 8) * ii))[q] =
+                cmk((float)cn, (float)sn);
         }
     }
     for (int c = tid; c < W::CPWG; c += W::THREADS) {
@@ -480,20 +573,42 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         }
     };
     // rows of frame t live in buffer t&1: Y and gamma = max(|Y|^2 inv, eps)
-    // (the noise row itself for SS)
+    // (the noise row itself for SS); at 512 also d = max(gamma - 1, 0) and
+    // MMSE's (sqrt(pi)/2)/(gamma + 1e-12), or for SS P = |Y|^2, the unit
+    // phasor of Y in place of Y and 1/|Y| (gain output) — computed once here
+    // for the workgroup's cells instead of by each of them
     auto store_rows = [&](int t) {  // registers -> LDS rows of frame t
         if (t < nf) {
             float2* yrow = (float2*)(smem + W::OFF_Y + (t & 1) * W::YROW);
             float* grow = (float*)(smem + W::OFF_G + (t & 1) * W::GROW);
+            float2* grow2 = (float2*)grow;
+            float* arow = (float*)(smem + W::OFF_A + (t & 1) * W::AROW);
 #pragma unroll
             for (int u = 0; u < W::YPT; ++u) {
                 const int k = tid + u * W::THREADS;
                 if (k < B) {
-                    yrow[k] = py[u];
-                    if (ALGO == CSE_ALGO_SS)
-                        grow[k] = pn[u];
-                    else
-                        grow[k] = fmaxf((py[u].x * py[u].x + py[u].y * py[u].y) * pn[u], EPS);
+                    const float2 y = py[u];
+                    const float P = y.x * y.x + y.y * y.y;
+                    if (!W::R2) {
+                        yrow[k] = y;
+                        grow[k] = (ALGO == CSE_ALGO_SS) ? pn[u] : fmaxf(P * pn[u], EPS);
+                    } else if (ALGO == CSE_ALGO_SS) {
+                        // phasor y/|y| of the y rescaled by 2^64 below 2^-50
+                        // (v_rsq flushes denormals); (1, 0) where y = 0
+                        const float sc = fmaxf(fabsf(y.x), fabsf(y.y)) < 0x1p-50f ? 0x1p64f : 1.0f;
+                        const float yx = y.x * sc, yy = y.y * sc;
+                        const float pz = fmaf(yx, yx, yy * yy);
+                        const float r = __builtin_amdgcn_rsqf(pz);
+                        yrow[k] = pz > 0.0f ? make_float2(yx * r, yy * r) : make_float2(1.0f, 0.0f);
+                        grow2[k] = make_float2(pn[u], P);
+                        if (OUT) arow[k] = pz > 0.0f ? r * sc : 0.0f;
+                    } else {
+                        yrow[k] = y;
+                        const float gam = fmaxf(P * pn[u], EPS);
+                        grow2[k] = make_float2(gam, fmaxf(gam - 1.0f, 0.0f));
+                        if (ALGO == CSE_ALGO_MMSE)
+                            arow[k] = 0.88622692545275801f * fast_rcp(gam + 1e-12f);
+                    }
                 }
             }
         }
@@ -542,18 +657,17 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             {
                 const CellParam cpar = *(const CellParam*)(smem + W::OFF_CP + 32 * cslot);
                 const float alpha_t = (t == 0) ? 0.0f : cpar.p0;  // see gain_wiener
-                const cf base = *(const cf*)(smem + W::OFF_LC + 8 * i);
                 const int yb = W::OFF_Y + (t & 1) * W::YROW, gb = W::OFF_G + (t & 1) * W::GROW;
+                const int ab = W::OFF_A + (t & 1) * W::AROW;
                 // mirror halves: lane i's slot e (9 entries, 72 B) receives
                 // Z'[M - i - L e] (e < 8) and Z'[M/2] (e = 8); lane q takes
                 // z[s] (s >= 8) = Z'[q + L s] from lane (L - q) mod L, entry 15 - s
                 // (lane 0: its own entry 16 - s, entry 8 = Z'[M/2] for s = 8)
                 gain_pack<NFFT, ALGO, OUT>(
-                    (const float2*)(smem + yb + 8 * i), (const float*)(smem + gb + 4 * i),
-                    (const float2*)(smem + yb + 8 * (M - i - 7 * L)),
-                    (const float*)(smem + gb + 4 * (M - i - 7 * L)),
-                    (const float2*)(smem + yb + 8 * MH), (const float*)(smem + gb + 4 * MH), z,
-                    (cf*)(smem + creg + 72 * i), rr, alpha_t, cpar, base,
+                    (const float2*)(smem + yb), (const void*)(smem + gb),
+                    (const float*)(smem + ab), z, (cf*)(smem + creg + 72 * i), rr, alpha_t, cpar,
+                    (const float4*)(smem + W::OFF_LC + W::ROTSTR * i),
+                    (const cf*)(smem + W::OFF_LC + 8 * i),
                     (OUT && gout) ? gout + t * B : nullptr, i);
             }
             __builtin_amdgcn_s_setprio(0);
@@ -589,6 +703,15 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 // pass-1 twiddles e^{2πi i' b/M}, b = 1..15, of my column (per-lane
                 // row of 18 complex: 8 ds_read_b128), issued ahead of the DFT
                 const float4* twr = (const float4*)(smem + W::OFF_TW + 144 * i);
+#if CSE_JIT_TABLES
+                idft16(z);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float4 q4 = twr[k];
+                    z[2 * k + 1] = cmul(z[2 * k + 1], cmk(q4.x, q4.y));
+                    if (k < 7) z[2 * k + 2] = cmul(z[2 * k + 2], cmk(q4.z, q4.w));
+                }
+#else
                 float4 t4[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) t4[k] = twr[k];
@@ -599,6 +722,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     const cf t = ((b - 1) & 1) ? cmk(q4.z, q4.w) : cmk(q4.x, q4.y);
                     z[b] = cmul(z[b], t);
                 }
+#endif
                 }
             }
             CSE_MARK("pass2");
@@ -671,8 +795,11 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 wv[4 * k + 3] = q4.w;
             }
         }
-        auto win = [&](int q) {  // w(n)/NFFT at slot q (compile-time after unrolling)
-            return (W::HALF_TABLES && q >= 16) ? (1.0f / (float)M / 2.0f) - wv[q - 16] : wv[q];
+        // w(n)/(NFFT S(n)) at slot q (compile-time after unrolling); at 1024 S is
+        // constant and slot q + 16 is w(n + N/2)/(N S) = 1/(N S) - w(n)/(N S)
+        constexpr float KHALF = (float)(1.0 / (NFFT * (R == 8 ? 3.0 : 1.5)));
+        auto win = [&](int q) {
+            return (W::HALF_TABLES && q >= 16) ? KHALF - wv[q - 16] : wv[q];
         };
         float done[F];
 #pragma unroll
@@ -690,29 +817,15 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             const bool interior = !edge && lo + (lag < 0 ? lag : 0) >= 0 &&
                                   lo + HOP + (lag > 0 ? lag : 0) <= len;  // uniform
             const bool head = want_y && lo < out_len;                      // uniform
-            float inv[F];
-            if (R == 2) {
-                const float4* it = (const float4*)(smem + W::OFF_IWS + 4 * W::ISTR * i);
-#pragma unroll
-                for (int k = 0; k < F / 4; ++k) {
-                    const float4 q4 = it[k];
-                    inv[4 * k] = q4.x;
-                    inv[4 * k + 1] = q4.y;
-                    inv[4 * k + 2] = q4.z;
-                    inv[4 * k + 3] = q4.w;
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < F; ++q) inv[q] = (R == 4) ? (1.0f / 1.5f) : (1.0f / 3.0f);
-            }
             float part = 0.0f;
             if (interior) {
-                // steady state: every slot is inside [0, len); the finiteness
-                // check rides along as chk += y*0 (NaN for a NaN or inf y)
+                // steady state: every slot is inside [0, len) and the window
+                // already carries 1/wss; the finiteness check rides along as
+                // chk += y*0 (NaN for a NaN or inf y)
 #pragma unroll
                 for (int q = 0; q < F; ++q) {
                     const int n = SP * (q >> 1) + (q & 1);
-                    const float y = done[q] * inv[q];
+                    const float y = done[q];
                     chk = fmaf(y, 0.0f, chk);
                     if (head && yout && o0 + n < out_len) yout[o0 + n] = y;
                     const float2 c2 = *(const float2*)(crow_t + SP * (q >> 1));
@@ -724,18 +837,21 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 for (int q = 0; q < F; ++q) {
                     const int n = SP * (q >> 1) + (q & 1);  // + off: position inside frame t
                     const int o = o0 + n;
-                    float iv = inv[q];
-                    if (edge) {  // sum the windows of the frames that cover this sample
-                        float wss = 0.0f;
+                    float iv = 1.0f;
+                    if (edge) {
+                        // fewer than R frames cover this sample: librosa divides by
+                        // the covering frames' window-square sum, not S(n).  With
+                        // T_r = w_r/(N S) the table entries of the R frames,
+                        // S / sum_cov w_r^2 = sum_all T_r^2 / sum_cov T_r^2.
+                        float all = 0.0f, cov = 0.0f;
 #pragma unroll
                         for (int r = 0; r < R; ++r) {
+                            const float w = win(q + 2 * r * (HOP / SP));
+                            all = fmaf(w, w, all);
                             const int tr = t - r;
-                            if (tr >= 0 && tr < nf) {
-                                const float w = win(q + 2 * r * (HOP / SP)) * NFFT;
-                                wss = fmaf(w, w, wss);
-                            }
+                            if (tr >= 0 && tr < nf) cov = fmaf(w, w, cov);
                         }
-                        iv = wss > 0.0f ? __builtin_amdgcn_rcpf(wss) : 1.0f;
+                        iv = cov > 0.0f ? all * __builtin_amdgcn_rcpf(cov) : 1.0f;
                     }
                     if (o >= 0 && o < len) {
                         const float y = done[q] * iv;

@@ -14,10 +14,10 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-B512="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity"
-P512="bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-parity"
-B1024="bench.py --nfft 1024 --steps 3 --warmup 1 --no-cpu-baseline --no-parity"
-P1024="bench.py --nfft 1024 --steps 1 --warmup 0 --no-cpu-baseline --no-parity"
+B512="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity --full-grid-steps 0 --no-sweep"
+P512="bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-parity --full-grid-steps 0 --no-sweep"
+B1024="bench.py --nfft 1024 --steps 3 --warmup 1 --no-cpu-baseline --no-parity --full-grid-steps 0 --no-sweep"
+P1024="bench.py --nfft 1024 --steps 1 --warmup 0 --no-cpu-baseline --no-parity --full-grid-steps 0 --no-sweep"
 SWEEP="tools/bench_sweep.py --pairs 4 --reps 1"
 SQ1="SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
 SQ2="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"
