@@ -645,6 +645,22 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 
     for (int t = 0; t < nf + R - 1; ++t) {
         float x[32];  // this frame's windowed IFFT samples (0 in flush frames)
+        // the lane's window slots: ds_read_b128 from its 16-B aligned table row
+        // (issued before the pass-2 DFT instead: +0.7 % at 512, the 32 VGPRs
+        // held through it cost more than the latency they hide)
+        float wv[W::WSLOTS];
+        auto load_win = [&]() {
+            const float4* w4 = (const float4*)(smem + W::OFF_WIN + 4 * W::WSTR * i);
+#pragma unroll
+            for (int k = 0; k < W::WSLOTS / 4; ++k) {
+                const float4 q4 = w4[k];
+                wv[4 * k] = q4.x;
+                wv[4 * k + 1] = q4.y;
+                wv[4 * k + 2] = q4.z;
+                wv[4 * k + 3] = q4.w;
+            }
+        };
+
         if (t < nf) {
             // the one workgroup barrier per frame: rows(t) (stored during frame
             // t-1) are visible, and nobody still reads buffer (t+1)&1
@@ -778,25 +794,13 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         // slot q < F of this frame completes output position t*HOP + n(q):
         // y = (ola) / wss (librosa istft normalisation), then the SNR error
         // sum of the clipped sample (evaluation_metrics.py:52-56).  Steady
-        // frames use the closed-form wss; the first R-1 and the flush frames
-        // sum the covering windows explicitly.
-        // windowed overlap-add: x * w(n)/n_fft folded into the accumulating FMAs
-        // (x = 0 in flush frames, so they leave the sums unchanged)
-        // the lane's window slots: ds_read_b128 from its 16-B aligned table row
-        float wv[W::WSLOTS];
-        {
-            const float4* w4 = (const float4*)(smem + W::OFF_WIN + 4 * W::WSTR * i);
-#pragma unroll
-            for (int k = 0; k < W::WSLOTS / 4; ++k) {
-                const float4 q4 = w4[k];
-                wv[4 * k] = q4.x;
-                wv[4 * k + 1] = q4.y;
-                wv[4 * k + 2] = q4.z;
-                wv[4 * k + 3] = q4.w;
-            }
-        }
+        // frames divide by S(n) through the window table; the first R-1 and
+        // the flush frames by the covering frames' window-square sum.
+        // windowed overlap-add: x * w(n)/(n_fft S(n)) folded into the
+        // accumulating FMAs (x = 0 in flush frames: the sums stay unchanged)
         // w(n)/(NFFT S(n)) at slot q (compile-time after unrolling); at 1024 S is
         // constant and slot q + 16 is w(n + N/2)/(N S) = 1/(N S) - w(n)/(N S)
+        load_win();
         constexpr float KHALF = (float)(1.0 / (NFFT * (R == 8 ? 3.0 : 1.5)));
         auto win = [&](int q) {
             return (W::HALF_TABLES && q >= 16) ? KHALF - wv[q - 16] : wv[q];
@@ -821,17 +825,30 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             if (interior) {
                 // steady state: every slot is inside [0, len) and the window
                 // already carries 1/wss; the finiteness check rides along as
-                // chk += y*0 (NaN for a NaN or inf y)
+                // chk += y*0 (NaN for a NaN or inf y).  Two accumulator chains
+                // each (even / odd slots): the frame's last dependent chain
+                // (one chain each: 24.51 -> two: 24.15 ms at 13 pairs)
+                float2 cl2[F / 2];  // the clean samples of slots q, q + 1
+#pragma unroll
+                for (int k = 0; k < F / 2; ++k) cl2[k] = *(const float2*)(crow_t + SP * k);
+                float pa = 0.0f, pb = 0.0f, ca = 0.0f, cb = 0.0f;
 #pragma unroll
                 for (int q = 0; q < F; ++q) {
                     const int n = SP * (q >> 1) + (q & 1);
                     const float y = done[q];
-                    chk = fmaf(y, 0.0f, chk);
                     if (head && yout && o0 + n < out_len) yout[o0 + n] = y;
-                    const float2 c2 = *(const float2*)(crow_t + SP * (q >> 1));
-                    const float d = ((q & 1) ? c2.y : c2.x) - fminf(fmaxf(y, -1.0f), 1.0f);
-                    part = fmaf(d, d, part);
+                    const float d = ((q & 1) ? cl2[q >> 1].y : cl2[q >> 1].x) -
+                                    fminf(fmaxf(y, -1.0f), 1.0f);
+                    if (q & 1) {
+                        cb = fmaf(y, 0.0f, cb);
+                        pb = fmaf(d, d, pb);
+                    } else {
+                        ca = fmaf(y, 0.0f, ca);
+                        pa = fmaf(d, d, pa);
+                    }
                 }
+                part = pa + pb;
+                chk += ca + cb;
             } else {
 #pragma unroll
                 for (int q = 0; q < F; ++q) {
