@@ -110,7 +110,9 @@ __device__ __forceinline__ float mmse_bracket(float v, float sqrtv) {
 __device__ __forceinline__ float gain_wiener(float gam, float d, float& rr, float alpha_t,
                                              float gfloor) {
     const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * d, 1e-10f);
-    const float g = fminf(fmaxf(xi * fast_rcp(1.0f + xi), gfloor), 1.0f);
+    // np.clip as one v_med3; gfloor arrives as min(gain_floor, 1), numpy's
+    // result when the bounds cross
+    const float g = __builtin_amdgcn_fmed3f(xi * fast_rcp(1.0f + xi), gfloor, 1.0f);
     rr = (g * g) * gam;
     return g;
 }
@@ -124,8 +126,10 @@ __device__ __forceinline__ float gain_mmse(float gam, float d, float cig, float&
     const float h = mmse_bracket(v, sv);
     float g = (sv * cig) * h;
     // nan_to_num(nan -> gmin, +inf -> gmax, -inf -> gmin) + clip (mmse.py:98-104):
-    // fmaxf returns the non-NaN operand, so the clip alone does all of it.
-    g = fminf(fmaxf(g, gmin), gmax);
+    // g is finite for finite input (v is clipped, cig finite), so the clip is
+    // one v_med3 (gmin arrives as min(gain_min, gain_max): numpy's clip gives
+    // gain_max when the bounds cross)
+    g = __builtin_amdgcn_fmed3f(g, gmin, gmax);
     rr = (g * g) * gam;
     return g;
 }
@@ -141,8 +145,9 @@ __device__ __forceinline__ float gain_mmse(float gam, float d, float cig, float&
 // 0 <= X <= 1e6, so lg is finite or -inf (xi = 0 with ksi_min = 0), and -inf
 // gives g = exp2(-inf) = 0 -> clip -> gain_floor, the reference's 0**p * gf**(1-p)
 // clipped (p >= 1e-10 > 0).  Non-finite input makes the cell non-finite either way.
+// gclip = min(gain_floor, 1): the lower bound of the final np.clip
 __device__ __forceinline__ float gain_omlsa(float gam, float d, float& rr, float alpha_t,
-                                            float ksi_min, float gfloor, float lg2_floor, float q,
+                                            float ksi_min, float gclip, float lg2_floor, float q,
                                             float vmax) {
     const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * d, ksi_min);
     const float r = fast_rcp(1.0f + xi);
@@ -157,7 +162,7 @@ __device__ __forceinline__ float gain_omlsa(float gam, float d, float& rr, float
     // reference's clip (advanced_mmse.py:116) needs no instruction
     const float p = A * fast_rcp(A + (1.0f - q));
     const float g = fast_exp2(lg2_floor + p * (lg - lg2_floor));
-    const float G = __builtin_amdgcn_fmed3f(g, gfloor, 1.0f);  // g >= 0, never NaN
+    const float G = __builtin_amdgcn_fmed3f(g, gclip, 1.0f);  // g >= 0, never NaN
     rr = (G * G) * gam;
     return G;
 }
@@ -276,7 +281,7 @@ __device__ __forceinline__ void wave_sync() {
 
 // per-cell parameters as the gain stage wants them
 struct CellParam {
-    float p0, p1, p2, p3, p4, lg2_floor, q_spp, pad;
+    float p0, p1, p2, p3, p4, lg2_floor, q_spp, gclip;  // gclip: OMLSA min(gain_floor, 1)
 };
 static_assert(sizeof(CellParam) == 32, "CellParam layout");
 
@@ -326,7 +331,7 @@ __device__ __forceinline__ cf gain_bin(float2 y, RowV rv, float& rr, float alpha
         const float cig = R2 ? rv.a : 0.88622692545275801f * fast_rcp(rv.g + 1e-12f);
         g = gain_mmse(rv.g, d, cig, rr, alpha_t, cp.p1, cp.p2, cp.p3);
     } else {
-        g = gain_omlsa(rv.g, d, rr, alpha_t, cp.p1, cp.p2, cp.lg2_floor, cp.q_spp, cp.p4);
+        g = gain_omlsa(rv.g, d, rr, alpha_t, cp.p1, cp.gclip, cp.lg2_floor, cp.q_spp, cp.p4);
     }
     return cmk(y.x * g, y.y * g);
 }
@@ -544,7 +549,12 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         prm.p4 = cp->param[4];
         prm.lg2_floor = (ALGO == CSE_ALGO_OMLSA) ? fast_log2(prm.p2) : 0.0f;
         prm.q_spp = fminf(fmaxf(prm.p3, 1e-3f), 1.0f - 1e-3f);
-        prm.pad = 0.0f;
+        prm.gclip = 0.0f;
+        // clip bounds for one v_med3: the lower bound capped at the upper one
+        // (numpy's clip returns the upper bound when they cross)
+        if (ALGO == CSE_ALGO_WIENER) prm.p1 = fminf(prm.p1, 1.0f);
+        if (ALGO == CSE_ALGO_MMSE) prm.p2 = fminf(prm.p2, prm.p3);
+        if (ALGO == CSE_ALGO_OMLSA) prm.gclip = fminf(prm.p2, 1.0f);
         ((CellParam*)(smem + W::OFF_CP))[c] = prm;
     }
 
@@ -837,8 +847,10 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     const int n = SP * (q >> 1) + (q & 1);
                     const float y = done[q];
                     if (head && yout && o0 + n < out_len) yout[o0 + n] = y;
+                    // np.clip as one v_med3 (fminf(fmaxf()) of a value carried
+                    // across the loop got a canonicalising v_max in front)
                     const float d = ((q & 1) ? cl2[q >> 1].y : cl2[q >> 1].x) -
-                                    fminf(fmaxf(y, -1.0f), 1.0f);
+                                    __builtin_amdgcn_fmed3f(y, -1.0f, 1.0f);
                     if (q & 1) {
                         cb = fmaf(y, 0.0f, cb);
                         pb = fmaf(d, d, pb);
@@ -875,7 +887,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                         if (head && yout && o < out_len) yout[o] = y;
                         if (o + lag >= 0 && o + lag < len) {  // dropped by the alignment otherwise
                             chk = fmaf(y, 0.0f, chk);
-                            const float d = crow_t[n] - fminf(fmaxf(y, -1.0f), 1.0f);
+                            const float d = crow_t[n] - __builtin_amdgcn_fmed3f(y, -1.0f, 1.0f);
                             part = fmaf(d, d, part);
                         }
                     }
