@@ -456,7 +456,9 @@ def main():
                 "units_per_step": f_units, "cells_per_step": 9744 * total_pairs,
                 "steps": fsteps, "warmup": 1, "ms_per_step": fdt / fsteps * 1e3,
                 "kernel_ms": {str(p.n_fft): k for p, k in zip(fjob.mps[0].plans, fkern)},
-                "units_per_launch_rank0": {str(p.n_fft): p.units for p in fjob.mps[0].plans}}
+                "units_per_launch_rank0": {str(p.n_fft): p.units for p in fjob.mps[0].plans},
+                "roofline": {str(p.n_fft): roofline_block(p.n_fft, p.units, k)
+                             for p, k in zip(fjob.mps[0].plans, fkern)}}
         del fjob, f_clean, f_noisy
 
     # ---- sweep: the reference's whole job (speech_enhancement_comparison.py:441-455 ->
