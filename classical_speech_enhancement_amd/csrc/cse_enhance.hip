@@ -136,11 +136,16 @@ __device__ __forceinline__ float gain_mmse(float gam, float d, float cig, float&
 
 // Log-MMSE x speech-presence gain (advanced_mmse.py:100-121), in the log2 domain:
 //   log2 g_lsa = log2(xi/(1+xi)) + 0.5 log2(e) E1(v)
-//             = log2(xi r / sqrt(vc)) + Q(vc),  vc = min(v, 11)
-//   with Q = 0.5 log2(e) (Ein - gamma_E) (tools/gen_special.py); for v >= 11 this
-//   differs from the exact form by 0.5 log2(e)(E1(11) - E1(v)) < 1.1e-6, no branch.
+//             = log2(xi r / sqrt(vc)) + Q(vc),  vc = min(v, 11.5)
+//   with Q = 0.5 log2(e) (Ein - gamma_E) = Pn(vc)/Dn(vc), a (4, 3) rational
+//   (tools/gen_special.py); for v >= 11.5 this differs from the exact form by
+//   0.5 log2(e)(E1(11.5) - E1(v)) < 6e-7, no branch.
 //   p = 1/(1 + (1-q)/(q Lambda + eps)) = A / (A + 1 - q),  A = q Lambda + eps
 //   G = clip(g_lsa^p gf^(1-p), gf, 1) = clip(exp2(lgf + p (lg - lgf)), gf, 1)
+//   p (lg - lgf) = A ((L - lgf) Dn + Pn) / ((A + 1 - q) Dn),  L = log2(xi r / sqrt(vc)):
+//   the rational's quotient and p share one reciprocal (8 VALU for Q where a
+//   degree-11 polynomial took 12).  Dn lies in [0.045, 1] and A <= e^80, so
+//   neither (A + 1 - q) Dn nor A ((L - lgf) Dn + Pn) overflows.
 // nan_to_num of g_lsa (advanced_mmse.py:106) needs no code: for finite input
 // 0 <= X <= 1e6, so lg is finite or -inf (xi = 0 with ksi_min = 0), and -inf
 // gives g = exp2(-inf) = 0 -> clip -> gain_floor, the reference's 0**p * gf**(1-p)
@@ -154,14 +159,16 @@ __device__ __forceinline__ float gain_omlsa(float gam, float d, float& rr, float
     const float xr = xi * r;
     const float v = __builtin_amdgcn_fmed3f(xr * gam, 1e-12f, vmax);
     const float vc = fminf(v, CSE_LSA_VMAX);
-    const float Q = horner(CSE_LSAQ, fmaf(vc, 2.0f / CSE_LSA_VMAX, -1.0f));
-    const float lg = fast_log2(xr * __builtin_amdgcn_rsqf(vc)) + Q;
+    const float pn = horner(CSE_LSAP, vc);
+    const float dn = horner(CSE_LSAD, vc);
+    const float L = fast_log2(xr * __builtin_amdgcn_rsqf(vc));
     const float ev = fast_exp2(v * kLog2e);
     const float A = q * (r * ev) + 1e-10f;
-    // A >= 1e-10 and 1 - q > 0: p lies in (0, 1) up to one rounding, so the
-    // reference's clip (advanced_mmse.py:116) needs no instruction
-    const float p = A * fast_rcp(A + (1.0f - q));
-    const float g = fast_exp2(lg2_floor + p * (lg - lg2_floor));
+    // A >= 1e-10 and 1 - q > 0: p = A/(A + 1 - q) lies in (0, 1) up to a rounding,
+    // so the reference's clip (advanced_mmse.py:116) needs no instruction
+    const float num = fmaf(L - lg2_floor, dn, pn);
+    const float den = (A + (1.0f - q)) * dn;
+    const float g = fast_exp2(fmaf(A * num, fast_rcp(den), lg2_floor));
     const float G = __builtin_amdgcn_fmed3f(g, gclip, 1.0f);  // g >= 0, never NaN
     rr = (G * G) * gam;
     return G;
