@@ -146,31 +146,37 @@ __device__ __forceinline__ float gain_mmse(float gam, float d, float cig, float&
 //   the rational's quotient and p share one reciprocal (8 VALU for Q where a
 //   degree-11 polynomial took 12).  Dn lies in [0.045, 1] and A <= e^80, so
 //   neither (A + 1 - q) Dn nor A ((L - lgf) Dn + Pn) overflows.
+// The bin works on v' = v log2(e), the exp2 argument of Lambda: gam2 = gamma
+// log2(e) (the n_fft 512 stager stores it so), the decision-directed state
+// rr = G^2 gam2 (so its weight is alpha ln 2), the rational in v' and
+// L' = log2(xr rsq(v')) = L - 0.5 log2(log2 e), the constant folded into lgf_c.
+constexpr float kLn2 = 0.69314718055994531f;
+constexpr float kLsaC = 0.26438318647244886f;  // 0.5 log2(log2 e)
 // nan_to_num of g_lsa (advanced_mmse.py:106) needs no code: for finite input
 // 0 <= X <= 1e6, so lg is finite or -inf (xi = 0 with ksi_min = 0), and -inf
 // gives g = exp2(-inf) = 0 -> clip -> gain_floor, the reference's 0**p * gf**(1-p)
 // clipped (p >= 1e-10 > 0).  Non-finite input makes the cell non-finite either way.
 // gclip = min(gain_floor, 1): the lower bound of the final np.clip
-__device__ __forceinline__ float gain_omlsa(float gam, float d, float& rr, float alpha_t,
-                                            float ksi_min, float gclip, float lg2_floor, float q,
-                                            float vmax) {
-    const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * d, ksi_min);
+__device__ __forceinline__ float gain_omlsa(float gam2, float d, float& rr, float a_rr, float a_d,
+                                            float ksi_min, float gclip, float lg2_floor,
+                                            float lgf_c, float q, float vmax2) {
+    const float xi = fmaxf(a_rr * rr + a_d * d, ksi_min);
     const float r = fast_rcp(1.0f + xi);
     const float xr = xi * r;
-    const float v = __builtin_amdgcn_fmed3f(xr * gam, 1e-12f, vmax);
-    const float vc = fminf(v, CSE_LSA_VMAX);
-    const float pn = horner(CSE_LSAP, vc);
-    const float dn = horner(CSE_LSAD, vc);
-    const float L = fast_log2(xr * __builtin_amdgcn_rsqf(vc));
-    const float ev = fast_exp2(v * kLog2e);
+    const float v2 = __builtin_amdgcn_fmed3f(xr * gam2, 1e-12f * kLog2e, vmax2);
+    const float vc2 = fminf(v2, CSE_LSA_VMAX2);
+    const float pn = horner(CSE_LSAP, vc2);
+    const float dn = horner(CSE_LSAD, vc2);
+    const float L = fast_log2(xr * __builtin_amdgcn_rsqf(vc2));
+    const float ev = fast_exp2(v2);
     const float A = q * (r * ev) + 1e-10f;
     // A >= 1e-10 and 1 - q > 0: p = A/(A + 1 - q) lies in (0, 1) up to a rounding,
     // so the reference's clip (advanced_mmse.py:116) needs no instruction
-    const float num = fmaf(L - lg2_floor, dn, pn);
+    const float num = fmaf(L - lgf_c, dn, pn);
     const float den = (A + (1.0f - q)) * dn;
     const float g = fast_exp2(fmaf(A * num, fast_rcp(den), lg2_floor));
     const float G = __builtin_amdgcn_fmed3f(g, gclip, 1.0f);  // g >= 0, never NaN
-    rr = (G * G) * gam;
+    rr = (G * G) * gam2;
     return G;
 }
 
@@ -293,7 +299,7 @@ struct CellParam {
 static_assert(sizeof(CellParam) == 32, "CellParam layout");
 
 // One bin's shared row values (staged once per workgroup and frame):
-//   Wiener/MMSE/OMLSA: g = gamma, d = max(gamma - 1, 0) (512; 1024 computes d
+//   Wiener/MMSE/OMLSA: g = gamma (OMLSA at 512: gamma log2(e)), d = max(gamma - 1, 0) (512; 1024 computes d
 //     here), a = (sqrt(pi)/2)/(gamma + 1e-12) (MMSE at 512);
 //   SS at 512: g = N, d = P = |Y|^2, a = 1/|Y| (gain output only), and the Y
 //     row holds the unit phasor of Y instead of Y ((1, 0) where Y = 0);
@@ -302,9 +308,11 @@ struct RowV {
     float g, d, a;
 };
 
+// Returns the real factor s with S = y s (y possibly replaced: SS at 1024 with
+// Y = 0); the packing forms the products inside its sums and differences.
 template <int NFFT, int ALGO>
-__device__ __forceinline__ cf gain_bin(float2 y, RowV rv, float& rr, float alpha_t,
-                                       const CellParam& cp, float& g) {
+__device__ __forceinline__ float gain_bin(float2& y, RowV rv, float& rr, float alpha_t,
+                                          const CellParam& cp, float& g) {
     constexpr bool R2 = (NFFT == 512);
     if (ALGO == CSE_ALGO_SS) {
         // Ps = max(P - a N, b N); |S| = sqrt(Ps) with the noisy phase
@@ -322,14 +330,15 @@ __device__ __forceinline__ cf gain_bin(float2 y, RowV rv, float& rr, float alpha
                          (tiny_ps ? 0x1p-32f : 1.0f);
         if (R2) {  // y is the phasor
             g = sp * rv.a;
-            return cmk(sp * y.x, sp * y.y);
+            return sp;
         }
         const float sc = fmaxf(fabsf(y.x), fabsf(y.y)) < 0x1p-50f ? 0x1p64f : 1.0f;
         const float yx = y.x * sc, yy = y.y * sc;
         const float pz = fmaf(yx, yx, yy * yy);
         const float u = sp * __builtin_amdgcn_rsqf(pz);
         g = (pz > 0.0f) ? u * sc : 0.0f;
-        return (pz > 0.0f) ? cmk(yx * u, yy * u) : cmk(sp, 0.0f);  // angle(0) = 0
+        y = (pz > 0.0f) ? make_float2(yx, yy) : make_float2(1.0f, 0.0f);  // angle(0) = 0
+        return (pz > 0.0f) ? u : sp;
     }
     const float d = R2 ? rv.d : fmaxf(rv.g - 1.0f, 0.0f);
     if (ALGO == CSE_ALGO_WIENER) {
@@ -338,9 +347,12 @@ __device__ __forceinline__ cf gain_bin(float2 y, RowV rv, float& rr, float alpha
         const float cig = R2 ? rv.a : 0.88622692545275801f * fast_rcp(rv.g + 1e-12f);
         g = gain_mmse(rv.g, d, cig, rr, alpha_t, cp.p1, cp.p2, cp.p3);
     } else {
-        g = gain_omlsa(rv.g, d, rr, alpha_t, cp.p1, cp.gclip, cp.lg2_floor, cp.q_spp, cp.p4);
+        // per-frame terms (alpha_t ln 2, 1 - alpha_t, ...) are common to the bins
+        const float gam2 = R2 ? rv.g : rv.g * kLog2e;
+        g = gain_omlsa(gam2, d, rr, alpha_t * kLn2, 1.0f - alpha_t, cp.p1, cp.gclip, cp.lg2_floor,
+                       cp.lg2_floor - kLsaC, cp.q_spp, cp.p4 * kLog2e);
     }
-    return cmk(y.x * g, y.y * g);
+    return g;
 }
 
 // One frame's gain stage + real-IFFT packing for one lane.
@@ -426,18 +438,21 @@ __device__ __forceinline__ void gain_pack(const float2* __restrict__ yrow,
             gan.a = WANT_A ? arow[M / 2] : 0.0f;
         }
         float g0, g1;
-        cf A = gain_bin<NFFT, ALGO>(ya, ga, rr[j], alpha_t, cpar, g0);
-        cf Bm = gain_bin<NFFT, ALGO>(yb, gb, rr[8 + j], alpha_t, cpar, g1);
+        const float sa = gain_bin<NFFT, ALGO>(ya, ga, rr[j], alpha_t, cpar, g0);
+        const float sb = gain_bin<NFFT, ALGO>(yb, gb, rr[8 + j], alpha_t, cpar, g1);
         if (OUT && gout_row) {
             gout_row[i + L * j] = g0;
             gout_row[M - i - L * j] = g1;
         }
         if (j == 0 && i == 0) {  // irfft ignores Im of DC and Nyquist
-            A.y = 0.0f;
-            Bm.y = 0.0f;
+            ya.y = 0.0f;
+            yb.y = 0.0f;
         }
-        const float sx = A.x + Bm.x, sy = A.y - Bm.y;
-        const float dx = A.x - Bm.x, dy = A.y + Bm.y;
+        // S = X_k + X*_{M-k}, D = X_k - X*_{M-k} with X_k = ya sa, X_{M-k} = yb sb:
+        // the X_k products ride in the FMAs (6 VALU instead of 8)
+        const float bx = yb.x * sb, by = yb.y * sb;
+        const float sx = fmaf(ya.x, sa, bx), sy = fmaf(ya.y, sa, -by);
+        const float dx = fmaf(ya.x, sa, -bx), dy = fmaf(ya.y, sa, by);
         // packing rotor e^{2πi (i + L j)/NFFT}: the lane's table row, or base * W32^j
         cf w;
         if constexpr (WG<NFFT>::ROT_TABLE) {
@@ -458,9 +473,9 @@ __device__ __forceinline__ void gain_pack(const float2* __restrict__ yrow,
         }
     }
     float gm;
-    const cf Sm = gain_bin<NFFT, ALGO>(ya, ga, rr[16], alpha_t, cpar, gm);
+    const float sm = 2.0f * gain_bin<NFFT, ALGO>(ya, ga, rr[16], alpha_t, cpar, gm);
     if (OUT && gout_row && i == 0) gout_row[M / 2] = gm;
-    xw[8] = cmk(2.0f * Sm.x, -2.0f * Sm.y);
+    xw[8] = cmk(ya.x * sm, -ya.y * sm);
 }
 
 template <int NFFT, int HOP, int ALGO, bool OUT>
@@ -622,7 +637,9 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     } else {
                         yrow[k] = y;
                         const float gam = fmaxf(P * pn[u], EPS);
-                        grow2[k] = make_float2(gam, fmaxf(gam - 1.0f, 0.0f));
+                        // OMLSA's bins take gamma log2(e) (gain_omlsa), d from gamma
+                        grow2[k] = make_float2(ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam,
+                                               fmaxf(gam - 1.0f, 0.0f));
                         if (ALGO == CSE_ALGO_MMSE)
                             arow[k] = 0.88622692545275801f * fast_rcp(gam + 1e-12f);
                     }
