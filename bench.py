@@ -239,8 +239,11 @@ def rank_job(args, world, rank, n_fft):
 class TimedJob:
     """A rank's share of one step's work — STFT + noise PSDs, the fused enhance
     of every cell (one launch per n_fft), one all_gather of the per-cell records
-    — over device-resident pairs.  Two plan sets alternate: the next step's
-    analysis runs on a side stream under this step's enhance (no data shared)."""
+    and their copy to the host — over device-resident pairs.  Two plan sets
+    alternate: the next step's analysis runs on a side stream under this step's
+    enhance (no data shared).  With device collectives (RCCL, or world 1) the
+    records of step k reach pinned host memory on a copy stream while step k+1
+    computes; the timed region's closing synchronize covers the last copy."""
 
     def __init__(self, eng, noisy, clean, specs, gids, n_buf, align, dist_ctx):
         import torch
@@ -261,19 +264,33 @@ class TimedJob:
             t = torch.tensor([n_rec], dtype=torch.int64, device=self.coll_dev)
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
             n_rec = int(t.item())
-        # records: sse, finite, global cell id (-1: padding slot) per packed slot
-        self.rec_pad = torch.zeros((3, n_rec), dtype=torch.float64, device="cuda")
-        self.rec_pad[2] = -1.0
+        # records: sse, finite, global cell id (-1: padding slot) per packed slot,
+        # one set per plan set (a step's records are still being copied while
+        # the next step writes its own)
+        ids = torch.full((n_rec,), -1.0, dtype=torch.float64)
         o = 0
         for p in self.mps[0].plans:  # every plan set packs alike
             real = p.order >= 0
             g = np.full(p.n_packed, -1, dtype=np.int64)
             g[real] = np.asarray(gids, dtype=np.int64)[p.idx[p.order[real]]]
-            self.rec_pad[2, o:o + p.n_packed] = torch.as_tensor(g.astype(np.float64))
+            ids[o:o + p.n_packed] = torch.as_tensor(g.astype(np.float64))
             o += p.n_packed
-        self.rec_all = torch.empty((self.world * 3, n_rec), dtype=torch.float64,
-                                   device=self.coll_dev)
+        self.rec_pad = []
+        for _ in range(n_buf):
+            r = torch.zeros((3, n_rec), dtype=torch.float64, device="cuda")
+            r[2] = ids.to("cuda")
+            self.rec_pad.append(r)
+        self.rec_all = [torch.empty((self.world * 3, n_rec), dtype=torch.float64,
+                                    device=self.coll_dev) for _ in range(n_buf)]
+        # device collectives: host copies ride a copy stream into pinned memory
+        self.async_host = self.dist is None or str(self.coll_dev).startswith("cuda")
+        if self.async_host:
+            self.copy_s = torch.cuda.Stream()
+            self.host_rec = [torch.empty((self.world * 3, n_rec), dtype=torch.float64,
+                                         pin_memory=True) for _ in range(n_buf)]
+            self.ev_copied = [None] * n_buf
         self.gathered = None
+        self.gathered_buf = None
         if n_buf > 1:
             self.prep(0)
 
@@ -308,22 +325,38 @@ class TimedJob:
         self.ev_done[b].record(self.main_s)
         if self.n_buf > 1:
             self.prep(self.k)  # overlaps this step's enhance (the timed region holds K preps)
+        rec = self.rec_pad[b]
+        if self.async_host and self.ev_copied[b] is not None:
+            self.main_s.wait_event(self.ev_copied[b])  # the copy that last read rec[b]
         o = 0
         for plan in mp.plans:
             m = plan.n_packed
-            self.rec_pad[0, o:o + m] = plan.sse_d
-            self.rec_pad[1, o:o + m] = plan.fin_d
+            rec[0, o:o + m] = plan.sse_d
+            rec[1, o:o + m] = plan.fin_d
             o += m
         if self.dist is not None:
-            self.dist.all_gather_into_tensor(self.rec_all, self.rec_pad.to(self.coll_dev))
-            self.gathered = self.rec_all.cpu()
+            self.dist.all_gather_into_tensor(self.rec_all[b], rec.to(self.coll_dev))
+            src = self.rec_all[b]
         else:
-            self.gathered = self.rec_pad.cpu()
+            src = rec
+        if self.async_host:
+            ev = torch.cuda.Event()
+            ev.record(self.main_s)
+            self.copy_s.wait_event(ev)
+            with torch.cuda.stream(self.copy_s):
+                self.host_rec[b].copy_(src, non_blocking=True)
+            self.ev_copied[b] = torch.cuda.Event()
+            self.ev_copied[b].record(self.copy_s)
+            self.gathered, self.gathered_buf = self.host_rec[b], b
+        else:
+            self.gathered = src.cpu()
         return self.gathered
 
     def table(self, n_cells):
         """The last step's gathered records as [n_cells, 2] (sse, finite) by
         global cell id; every cell exactly once."""
+        if self.async_host:
+            self.ev_copied[self.gathered_buf].synchronize()
         r = self.gathered.numpy().reshape(self.world, 3, -1).transpose(1, 0, 2).reshape(3, -1)
         ids = r[2].astype(np.int64)
         keep = ids >= 0
