@@ -208,7 +208,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 template <int NFFT>
 struct WG {
     using G = Geo<NFFT>;
-    static constexpr int WAVES = CSE_WG_WAVES;
+    static constexpr int WAVES = NFFT == 512 ? CSE_WG_WAVES : CSE_WG_WAVES_1024;
     static constexpr int THREADS = 64 * WAVES;
     static constexpr int CPWG = WAVES * G::CPW;                   // cells per workgroup
     static constexpr int HMAX = 256;                              // largest hop
@@ -271,9 +271,11 @@ struct WG {
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
 // the registers (3 waves/SIMD) set the occupancy: LDS must not cut it below
-// 3 workgroups (12 waves) per CU
-static_assert(3 * WG<512>::BYTES <= 163840, "n_fft=512 workgroups must fit 3 per CU");
-static_assert(3 * WG<1024>::BYTES <= 163840, "n_fft=1024 workgroups must fit 3 per CU");
+// 12 waves (3 per SIMD) per CU
+static_assert((163840 / WG<512>::BYTES) * WG<512>::WAVES >= 12,
+              "n_fft=512 workgroups must fit 12 waves per CU");
+static_assert((163840 / WG<1024>::BYTES) * WG<1024>::WAVES >= 12,
+              "n_fft=1024 workgroups must fit 12 waves per CU");
 static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
               WG<1024>::CPWG == CSE_CELLS_PER_GROUP(1024), "cse.h slot-group size");
 
@@ -949,7 +951,10 @@ __device__ __forceinline__ void dispatch_algo(const Args& a, const cse_cell_t* w
 // OUT: the g_out (gain matrix) variant for parity tests; waveform output
 // (y_out, any out_len) is available in both variants at run time.
 template <int NFFT, bool OUT>
-__global__ void __launch_bounds__(WG<NFFT>::THREADS, CSE_WAVES_PER_SIMD) enhance_kernel(Args a) {
+// launch bounds: workgroups per CU such that the register budget allows
+// CSE_WAVES_PER_SIMD waves per SIMD (4 SIMDs per CU)
+__global__ void __launch_bounds__(WG<NFFT>::THREADS, 4 * CSE_WAVES_PER_SIMD / WG<NFFT>::WAVES)
+    enhance_kernel(Args a) {
     using W = WG<NFFT>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wg = xcd_remap(blockIdx.x, gridDim.x);

@@ -61,7 +61,7 @@ enum {
 /*
  * One grid cell = one (signal group, noise PSD, algorithm, parameter set).
  * Cells are processed CSE_CELLS_PER_GROUP(n_fft) at a time by one workgroup of
- * CSE_WG_WAVES wavefronts (4: 256 threads) that stages their shared rows in LDS, so the cells
+ * CSE_WG_WAVES (n_fft 512) / CSE_WG_WAVES_1024 wavefronts that stages their shared rows in LDS, so the cells
  * of one such slot group (cells[g*G .. g*G+G-1]) MUST share algo, hop,
  * y_offset, noise_offset, noise_stride, clean_offset and lag; pad a short
  * group with CSE_ALGO_NONE slots.  Only param, out_offset and gain_offset may
@@ -86,9 +86,12 @@ typedef struct cse_cell {
 } cse_cell_t;              /* 96 bytes */
 
 #ifndef CSE_WG_WAVES
-#define CSE_WG_WAVES 4 /* wavefronts per workgroup of the build (cse_cells_per_group reports it) */
+#define CSE_WG_WAVES 4 /* wavefronts per n_fft=512 workgroup (cse_cells_per_group reports it) */
 #endif
-#define CSE_CELLS_PER_GROUP(n_fft) ((n_fft) == 512 ? 4 * CSE_WG_WAVES : 2 * CSE_WG_WAVES)
+#ifndef CSE_WG_WAVES_1024
+#define CSE_WG_WAVES_1024 4 /* wavefronts per n_fft=1024 workgroup */
+#endif
+#define CSE_CELLS_PER_GROUP(n_fft) ((n_fft) == 512 ? 4 * CSE_WG_WAVES : 2 * CSE_WG_WAVES_1024)
 
 /* Library identity. */
 int cse_version(void);
