@@ -579,6 +579,11 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         if (ALGO == CSE_ALGO_WIENER) prm.p1 = fminf(prm.p1, 1.0f);
         if (ALGO == CSE_ALGO_MMSE) prm.p2 = fminf(prm.p2, prm.p3);
         if (ALGO == CSE_ALGO_OMLSA) prm.gclip = fminf(prm.p2, 1.0f);
+        // v enters the OMLSA gain only through e^v (the E1 term takes min(v, 11.5)),
+        // and at v = 80 the speech-presence p = A/(A + 1 - q) is already 1 in fp32
+        // (A >= 1e-3 e^80 / (1 + 1e16)): v_max beyond 80 changes nothing but
+        // would overflow e^v (fp32 max e^88.7), so it is capped here
+        if (ALGO == CSE_ALGO_OMLSA) prm.p4 = fminf(prm.p4, 80.0f);
         ((CellParam*)(smem + W::OFF_CP))[c] = prm;
     }
 

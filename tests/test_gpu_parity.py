@@ -169,6 +169,22 @@ def test_gain_matrices_match_oracle_gains():
         assert np.max(np.abs(Gd - ref)) < 1e-4, alg
 
 
+@pytest.mark.parametrize("v_max", [5.0, 20.0, 80.0, 150.0])
+def test_omlsa_v_max_against_oracle(P, v_max):
+    """OMLSA's v_max (advanced_mmse.py signature default 80, not swept by the
+    grid) below the LSA clamp, between it and 80, and beyond fp32's e^v range
+    (the kernel caps it at 80, where p = 1 in fp32 already): enhanced waveform
+    vs the fp64 oracle."""
+    _, noisy = make_pair(3, seconds=1.5)
+    for n_fft, hop in ((512, 128), (1024, 256)):
+        kw = dict(CELLS["omlsa"], n_fft=n_fft, hop_length=hop, noise_percentile=20.0,
+                  noise_method="min_tracking", v_max=v_max)
+        y = P.advanced_mmse(noisy, 16000, **kw)
+        ref = oracle.advanced_mmse(noisy, 16000, **kw)
+        assert np.all(np.isfinite(y))
+        assert rel_l2(y, ref) <= TOL and rel_max(y, ref) <= TOL, (n_fft, rel_l2(y, ref))
+
+
 def test_grid_snr_table_matches_reference(P):
     """Full HEAD grid on a 0.5-s pair: per-cell SNR of the clipped waveform."""
     import torch
