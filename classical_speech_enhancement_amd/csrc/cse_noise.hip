@@ -76,22 +76,25 @@ __device__ double lerp_percentile(const double* s, int n, double q) {
     return a + diff * gamma;
 }
 
-// mean_b log(max(P[t][b], eps)) per frame
-__global__ void frame_energy_kernel(const double* __restrict__ P, int T, int B, double eps,
-                                    double* __restrict__ energy) {
-    __shared__ double part[256];
-    const int t = blockIdx.x;
+// mean_b log(max(P[t][b], eps)) per frame: one wavefront per frame (4 per
+// 256-thread block), lane sums over b = lane + 64 m, then a butterfly
+// reduction (every lane ends with the same sum; no LDS, no block barrier).
+// The addition order is not numpy's pairwise one (neither was the r01-r03
+// block tree): the energies only rank frames, and frames with equal rows get
+// equal energies in any fixed order.
+__global__ void __launch_bounds__(256) frame_energy_kernel(const double* __restrict__ P, int T,
+                                                           int B, double eps,
+                                                           double* __restrict__ energy) {
+    const int lane = threadIdx.x & 63;
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t sig = blockIdx.y;
+    if (t >= T) return;  // whole wavefronts only
     const double* row = P + (sig * T + t) * (int64_t)B;
     double s = 0.0;
-    for (int b = threadIdx.x; b < B; b += blockDim.x) s += log(fmax(row[b], eps));
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) energy[sig * T + t] = part[0] / (double)B;
+    for (int b = lane; b < B; b += 64) s += log(fmax(row[b], eps));
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
+    if (lane == 0) energy[sig * T + t] = s / (double)B;
 }
 
 // k quietest frames: argsort(energy)[:k], ties by frame index.  Only the
@@ -148,6 +151,130 @@ __global__ void select_quiet_kernel(const double* __restrict__ energy, int T, in
 }
 
 enum { STATS_MEDIAN = 0, STATS_PERCENTILE = 1, STATS_SIMPLE = 2 };
+
+// ---------------------------------------------------------------------------
+// Per-wavefront bitonic sort of 64 E doubles held in registers, element
+// i = lane E + e in register e: exchanges at distance j < E stay inside the
+// lane (compile-time register pairs), j >= E cross lanes (lane ^ j/E, one
+// 64-bit shuffle per register).  No LDS and no block barrier: a 2048-element
+// column sorts in 66 stages of register min/max instead of 66 workgroup-wide
+// LDS rounds.  Ascending; values only (equal keys are interchangeable).
+// ---------------------------------------------------------------------------
+template <int E>
+__device__ __forceinline__ void wave_bitonic(double (&v)[E], int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64 * E; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j < E) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    if (e & j) continue;
+                    // i = lane E + e, partner i ^ j = lane E + (e ^ j) > i
+                    const bool up = (k < E) ? ((e & k) == 0) : ((lane & (k / E)) == 0);
+                    const double a = v[e], b = v[e | j];
+                    const double lo = fmin(a, b), hi = fmax(a, b);
+                    v[e] = up ? lo : hi;
+                    v[e | j] = up ? hi : lo;
+                }
+            } else {
+                const int d = j / E;
+                const bool first = (lane & d) == 0;      // i < partner
+                const bool up = (lane & (k / E)) == 0;  // k > j >= E
+                const bool take_min = first == up;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const double o = __shfl_xor(v[e], d, 64);
+                    v[e] = take_min ? fmin(v[e], o) : fmax(v[e], o);
+                }
+            }
+        }
+    }
+}
+
+// element idx of the wave-sorted array, broadcast to every lane
+template <int E>
+__device__ __forceinline__ double wave_at(const double (&v)[E], int lane, int idx) {
+    double r = 0.0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) r = (lane * E + e == idx) ? v[e] : r;
+    return __shfl(r, idx / E, 64);
+}
+
+// bin_stats_kernel's median / percentile modes for n2 = 64 E <= 2048 sort
+// slots: one wavefront per (bin, signal), 4 bins per block, the same order
+// statistics and the same arithmetic as the LDS path (bit-identical results)
+template <int E>
+__global__ void __launch_bounds__(256) bin_stats_wave_kernel(
+    const double* __restrict__ P, int T, int B, int mode, const int* __restrict__ sel, int k,
+    double q, double floor_rel, double eps, double* __restrict__ med, float* __restrict__ N) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t sig = blockIdx.y;
+    if (b >= B) return;  // whole wavefronts only
+    const double* Ps = P + sig * (int64_t)T * B + b;
+    const int n = (mode == STATS_MEDIAN) ? T : k;
+    const int* sl = sel ? sel + sig * (int64_t)T : nullptr;
+    double v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        const int t = i < n ? (mode == STATS_MEDIAN ? i : sl[i]) : 0;
+        v[e] = i < n ? Ps[(int64_t)t * B] : INFINITY;
+    }
+    wave_bitonic<E>(v, lane);
+    if (mode == STATS_MEDIAN) {
+        const double m = (T & 1) ? wave_at<E>(v, lane, T / 2)
+                                 : (wave_at<E>(v, lane, T / 2 - 1) + wave_at<E>(v, lane, T / 2)) / 2.0;
+        if (lane == 0) med[sig * B + b] = m;
+        return;
+    }
+    // np.percentile(..., q, method='linear') as lerp_percentile
+    const double virt = (double)(n - 1) * q;
+    double prev_f = floor(virt);
+    int prev, next;
+    if (virt >= (double)(n - 1)) {
+        prev = next = n - 1;
+        prev_f = -1.0;
+    } else if (virt < 0.0) {
+        prev = next = 0;
+        prev_f = 0.0;
+    } else {
+        prev = (int)prev_f;
+        next = prev + 1;
+    }
+    const double gamma = virt - prev_f;
+    const double a = wave_at<E>(v, lane, prev), c = wave_at<E>(v, lane, next);
+    const double diff = c - a;
+    const double pc = (gamma >= 0.5) ? c - diff * (1.0 - gamma) : a + diff * gamma;
+    const double est = fmax(pc, floor_rel * med[sig * B + b]);
+    if (lane == 0) N[sig * B + b] = (float)fmax(est, eps);
+}
+
+template <int E>
+static void launch_stats_wave(const double* P, int64_t n_sig, int T, int B, int mode,
+                              const int* sel, int k, double q, double floor_rel, double eps,
+                              double* med, float* N, hipStream_t s) {
+    hipLaunchKernelGGL(bin_stats_wave_kernel<E>, dim3((B + 3) / 4, (unsigned)n_sig), dim3(256), 0,
+                       s, P, T, B, mode, sel, k, q, floor_rel, eps, med, N);
+}
+
+// the wave path for n <= 2048 sort slots; false: use the LDS path
+static bool stats_wave(int n, const double* P, int64_t n_sig, int T, int B, int mode,
+                       const int* sel, int k, double q, double floor_rel, double eps, double* med,
+                       float* N, hipStream_t s) {
+    if (n > 2048 || n < 1) return false;
+    const int n2 = n <= 64 ? 64 : next_pow2(n);
+    switch (n2 / 64) {
+        case 1: launch_stats_wave<1>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, s); break;
+        case 2: launch_stats_wave<2>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, s); break;
+        case 4: launch_stats_wave<4>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, s); break;
+        case 8: launch_stats_wave<8>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, s); break;
+        case 16: launch_stats_wave<16>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, s); break;
+        default: launch_stats_wave<32>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, s); break;
+    }
+    return true;
+}
 
 // per (bin, signal): median over all frames (-> med), and optionally the
 // percentile over the selected quiet frames (-> N) or the T<5 simple estimate.
@@ -237,6 +364,67 @@ __global__ void min_filter_kernel(const double* __restrict__ S, int T, int B, in
         double m = Ss[(int64_t)lo * B];
         for (int u = lo + 1; u <= hi; ++u) m = fmin(m, Ss[(int64_t)u * B]);
         const double f = fmax(m, 0.01 * med[sig * B + b]);
+        N[(sig * T + t) * (int64_t)B + b] = (float)fmax(f, eps);
+        if (Nb) Nb[(sig * T + t) * (int64_t)B + b] = (float)fmax(f, eps_b);
+    }
+}
+
+// The same through an LDS tile (r03): a block owns 32 bins x 64 output frames
+// and stages rows t0 - half .. t0 + 63 + half (indices clamped to [0, T):
+// 'nearest' padding repeats the edge frames, which leaves the window minimum
+// unchanged); log2 doubling passes turn the tile into M_p[r] = min over rows
+// [r, r + p), p the largest power of two <= W = 2 half + 1, and each output is
+// min(M_p[r], M_p[r + W - p]) over its window [r, r + W).  About 7 LDS
+// operations per element instead of W = 51 global loads.  half <= MF_HMAX.
+constexpr int MF_T = 64, MF_B = 32, MF_HMAX = 25, MF_ROWS = MF_T + 2 * MF_HMAX;
+constexpr int MF_PER = (MF_ROWS + 7) / 8;  // tile rows per thread (8 row groups)
+__global__ void __launch_bounds__(256) min_filter_tiled_kernel(
+    const double* __restrict__ S, int T, int B, int half, const double* __restrict__ med,
+    double eps, float* __restrict__ N, double eps_b, float* __restrict__ Nb) {
+    __shared__ double tile[MF_ROWS][MF_B];
+    const int bl = threadIdx.x & (MF_B - 1), tg = threadIdx.x / MF_B;
+    const int b = blockIdx.x * MF_B + bl;
+    const int t0 = blockIdx.y * MF_T;
+    const int64_t sig = blockIdx.z;
+    const int rows = MF_T + 2 * half;
+    const double* Ss = S + sig * (int64_t)T * B;
+    const int bc = b < B ? b : B - 1;
+#pragma unroll
+    for (int m = 0; m < MF_PER; ++m) {
+        const int r = tg + 8 * m;
+        if (r < rows) {
+            const int t = min(max(t0 - half + r, 0), T - 1);
+            tile[r][bl] = Ss[(int64_t)t * B + bc];
+        }
+    }
+    const int W = 2 * half + 1;
+    int p = 1;
+    while (2 * p <= W) p *= 2;
+    for (int st = 1; st < p; st *= 2) {
+        __syncthreads();
+        double nv[MF_PER];
+#pragma unroll
+        for (int m = 0; m < MF_PER; ++m) {
+            const int r = tg + 8 * m;
+            nv[m] = (r + st < rows) ? fmin(tile[r][bl], tile[r + st][bl]) : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < MF_PER; ++m) {
+            const int r = tg + 8 * m;
+            if (r + st < rows) tile[r][bl] = nv[m];
+        }
+    }
+    __syncthreads();
+    if (b >= B) return;
+    const double fl = 0.01 * med[sig * B + b];
+#pragma unroll
+    for (int m = 0; m < MF_T / 8; ++m) {
+        const int r = tg + 8 * m;
+        const int t = t0 + r;
+        if (t >= T) break;
+        const double mn = fmin(tile[r][bl], tile[r + W - p][bl]);
+        const double f = fmax(mn, fl);
         N[(sig * T + t) * (int64_t)B + b] = (float)fmax(f, eps);
         if (Nb) Nb[(sig * T + t) * (int64_t)B + b] = (float)fmax(f, eps_b);
     }
@@ -369,6 +557,10 @@ static void quiet_count(int T, const cse_noise_params_t& prm, int* k_out, double
 
 static int launch_median(const double* P, int64_t n_sig, int T, int B, double* med,
                          hipStream_t s) {
+    if (stats_wave(T, P, n_sig, T, B, STATS_MEDIAN, nullptr, 0, 0.0, 0.0, 0.0, med, nullptr, s)) {
+        CSE_CHECK_LAUNCH("noise median");
+        return CSE_OK;
+    }
     const int n2_all = next_pow2(T);
     hipLaunchKernelGGL(bin_stats_kernel, dim3(B, (unsigned)n_sig), dim3(256),
                        (size_t)n2_all * sizeof(double), s, P, T, B, n2_all, (int)STATS_MEDIAN,
@@ -394,11 +586,16 @@ static int launch_percentile(const double* P, const double* med, int64_t n_sig, 
     double pct;
     quiet_count(T, prm, &k, &pct);
     const int n2_all = next_pow2(T), n2_sel = next_pow2(k);
-    hipLaunchKernelGGL(frame_energy_kernel, dim3(T, (unsigned)n_sig), dim3(256), 0, s, P, T, B,
-                       eps, w.energy);
+    hipLaunchKernelGGL(frame_energy_kernel, dim3((T + 3) / 4, (unsigned)n_sig), dim3(256), 0, s, P,
+                       T, B, eps, w.energy);
     hipLaunchKernelGGL(select_quiet_kernel, dim3((unsigned)n_sig), dim3(1024),
                        (size_t)n2_all * 8 + 1024 * 4, s, (const double*)w.energy, T, n2_all, k,
                        w.sel);
+    if (stats_wave(k, P, n_sig, T, B, STATS_PERCENTILE, (const int*)w.sel, k, pct / 100.0,
+                   prm.floor_rel, eps, (double*)med, N, s)) {
+        CSE_CHECK_LAUNCH("noise percentile");
+        return CSE_OK;
+    }
     hipLaunchKernelGGL(bin_stats_kernel, dim3(B, (unsigned)n_sig), dim3(256),
                        (size_t)n2_sel * sizeof(double), s, P, T, B, n2_all,
                        (int)STATS_PERCENTILE, (const int*)w.sel, k, n2_sel, pct / 100.0, prm.floor_rel,
@@ -419,8 +616,15 @@ static int launch_min_tracking(const double* P, const double* med, int64_t n_sig
     if (win % 2 == 0) win += 1;
     hipLaunchKernelGGL(iir_kernel, dim3(ceil_div(B, 64), (unsigned)n_sig), dim3(64), 0, s, P, T, B,
                        a, w.S);
-    hipLaunchKernelGGL(min_filter_kernel, dim3(T, (unsigned)n_sig), dim3(256), 0, s,
-                       (const double*)w.S, T, B, win / 2, med, eps, N, eps_b, Nb);
+    if (win / 2 <= MF_HMAX) {
+        hipLaunchKernelGGL(min_filter_tiled_kernel,
+                           dim3((B + MF_B - 1) / MF_B, (T + MF_T - 1) / MF_T, (unsigned)n_sig),
+                           dim3(256), 0, s, (const double*)w.S, T, B, win / 2, med, eps, N, eps_b,
+                           Nb);
+    } else {
+        hipLaunchKernelGGL(min_filter_kernel, dim3(T, (unsigned)n_sig), dim3(256), 0, s,
+                           (const double*)w.S, T, B, win / 2, med, eps, N, eps_b, Nb);
+    }
     CSE_CHECK_LAUNCH("noise min tracking");
     return CSE_OK;
 }

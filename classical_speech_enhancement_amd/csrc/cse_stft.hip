@@ -21,7 +21,13 @@ __device__ __forceinline__ int64_t reflect_index(int64_t p, int64_t len) {
     return q < len ? q : period - q;
 }
 
-// One workgroup per (frame, signal).  Radix-2 DIT FFT in LDS, fp64.
+// One workgroup per FPB consecutive frames of one signal.  Radix-2 DIT FFT in
+// LDS, fp64; the twiddles and the window are computed once per workgroup and
+// shared by its frames (r03: they were recomputed per frame, one fp64
+// sincospi / cospi per point), and only frames that reach past either end of
+// the signal take the 64-bit reflect arithmetic.  Every element sees the same
+// operations as before, so Y and P are bit-identical to the one-frame form.
+constexpr int STFT_FPB = 4;
 template <int NFFT>
 __global__ void __launch_bounds__(256) stft_kernel(const double* __restrict__ x,
                                                    const double* __restrict__ x_sub,
@@ -30,55 +36,66 @@ __global__ void __launch_bounds__(256) stft_kernel(const double* __restrict__ x,
                                                    double* __restrict__ P) {
     constexpr int LOG2N = (NFFT == 512) ? 9 : 10;
     constexpr int B = NFFT / 2 + 1;
-    __shared__ double re[NFFT], im[NFFT];
-    __shared__ double twr[NFFT / 2], twi[NFFT / 2];
-    const int t = blockIdx.x;
+    constexpr int F = STFT_FPB;
+    __shared__ double re[F][NFFT], im[F][NFFT];
+    __shared__ double twr[NFFT / 2], twi[NFFT / 2], win[NFFT];
+    const int tb = blockIdx.x * F;
+    const int nfr = min(F, T - tb);
     const int64_t sig = blockIdx.y;
     const double* xs = x + sig * len;
     const double* xd = x_sub ? x_sub + sig * len : nullptr;
     for (int k = threadIdx.x; k < NFFT / 2; k += blockDim.x) {
-        double s, c;
-        sincospi(-2.0 * (double)k / (double)NFFT, &s, &c);
+        double sn, c;
+        sincospi(-2.0 * (double)k / (double)NFFT, &sn, &c);
         twr[k] = c;
-        twi[k] = s;
+        twi[k] = sn;
     }
-    // load frame t of the reflect-padded signal, windowed, in bit-reversed order
-    for (int n = threadIdx.x; n < NFFT; n += blockDim.x) {
-        const int64_t p = (int64_t)t * hop + n - NFFT / 2;
-        const int64_t s = reflect_index(p, len);
-        double v = xs[s];
-        if (xd) v = v - xd[s];
-        const double w = 0.5 - 0.5 * cospi(2.0 * (double)n / (double)NFFT);
-        const int r = (int)(__brev((unsigned)n) >> (32 - LOG2N));
-        re[r] = v * w;
-        im[r] = 0.0;
+    for (int n = threadIdx.x; n < NFFT; n += blockDim.x)
+        win[n] = 0.5 - 0.5 * cospi(2.0 * (double)n / (double)NFFT);
+    __syncthreads();
+    // load the frames of the reflect-padded signal, windowed, in bit-reversed order
+    for (int f = 0; f < nfr; ++f) {
+        const int64_t p0 = (int64_t)(tb + f) * hop - NFFT / 2;
+        const bool inside = p0 >= 0 && p0 + NFFT <= len;  // uniform per frame
+        for (int n = threadIdx.x; n < NFFT; n += blockDim.x) {
+            const int64_t p = p0 + n;
+            const int64_t si = inside ? p : reflect_index(p, len);
+            double v = xs[si];
+            if (xd) v = v - xd[si];
+            const int r = (int)(__brev((unsigned)n) >> (32 - LOG2N));
+            re[f][r] = v * win[n];
+            im[f][r] = 0.0;
+        }
     }
     __syncthreads();
-    for (int s = 1; s <= LOG2N; ++s) {
-        const int half = 1 << (s - 1);
-        for (int b = threadIdx.x; b < NFFT / 2; b += blockDim.x) {
-            const int grp = b >> (s - 1);
+    for (int st = 1; st <= LOG2N; ++st) {
+        const int half = 1 << (st - 1);
+        for (int e = threadIdx.x; e < nfr * (NFFT / 2); e += blockDim.x) {
+            const int f = e / (NFFT / 2), b = e % (NFFT / 2);
+            const int grp = b >> (st - 1);
             const int j = b & (half - 1);
             const int i0 = grp * (half << 1) + j;
             const int i1 = i0 + half;
-            const int tw = j << (LOG2N - s);
+            const int tw = j << (LOG2N - st);
             const double wr = twr[tw], wi = twi[tw];
-            const double br = re[i1] * wr - im[i1] * wi;
-            const double bi = re[i1] * wi + im[i1] * wr;
-            const double ar = re[i0], ai = im[i0];
-            re[i0] = ar + br;
-            im[i0] = ai + bi;
-            re[i1] = ar - br;
-            im[i1] = ai - bi;
+            const double br = re[f][i1] * wr - im[f][i1] * wi;
+            const double bi = re[f][i1] * wi + im[f][i1] * wr;
+            const double ar = re[f][i0], ai = im[f][i0];
+            re[f][i0] = ar + br;
+            im[f][i0] = ai + bi;
+            re[f][i1] = ar - br;
+            im[f][i1] = ai - bi;
         }
         __syncthreads();
     }
-    const int64_t row = (sig * T + t) * (int64_t)B;
-    for (int k = threadIdx.x; k < B; k += blockDim.x) {
-        double r = re[k], i = im[k];
-        if (k == 0 || k == NFFT / 2) i = 0.0;  // pocketfft r2c: exact zero imag
-        if (Y) Y[row + k] = make_float2((float)r, (float)i);
-        if (P) P[row + k] = r * r + i * i;
+    for (int f = 0; f < nfr; ++f) {
+        const int64_t row = (sig * T + tb + f) * (int64_t)B;
+        for (int k = threadIdx.x; k < B; k += blockDim.x) {
+            double r = re[f][k], i = im[f][k];
+            if (k == 0 || k == NFFT / 2) i = 0.0;  // pocketfft r2c: exact zero imag
+            if (Y) Y[row + k] = make_float2((float)r, (float)i);
+            if (P) P[row + k] = r * r + i * i;
+        }
     }
 }
 
@@ -112,7 +129,7 @@ extern "C" int cse_stft(const double* x, const double* x_sub, int64_t n_sig, int
     CSE_CHECK_ARG(n_fft == 512 || n_fft == 1024, "cse_stft: n_fft=%d (512|1024)", n_fft);
     CSE_CHECK_ARG(hop >= 1 && hop <= n_fft, "cse_stft: hop=%d", hop);
     const int T = n_frames_for(len, hop);
-    dim3 grid(T, (unsigned)n_sig);
+    dim3 grid((unsigned)ceil_div(T, STFT_FPB), (unsigned)n_sig);
     if (n_fft == 512)
         hipLaunchKernelGGL(stft_kernel<512>, grid, dim3(256), 0, (hipStream_t)stream, x, x_sub,
                            len, hop, T, (float2*)Y, P);
