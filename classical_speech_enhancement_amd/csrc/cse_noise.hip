@@ -579,15 +579,20 @@ static int launch_simple(const double* P, int64_t n_sig, int T, int B, double ep
     return CSE_OK;
 }
 
-static int launch_percentile(const double* P, const double* med, int64_t n_sig, int T, int B,
-                             const cse_noise_params_t& prm, double eps, float* N, Workspace w,
-                             hipStream_t s) {
+static void launch_energy(const double* P, int64_t n_sig, int T, int B, double eps, Workspace w,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(frame_energy_kernel, dim3((T + 3) / 4, (unsigned)n_sig), dim3(256), 0, s, P,
+                       T, B, eps, w.energy);
+}
+
+// the percentile estimate from the frame energies already in w.energy
+static int launch_percentile_sel(const double* P, const double* med, int64_t n_sig, int T, int B,
+                                 const cse_noise_params_t& prm, double eps, float* N, Workspace w,
+                                 hipStream_t s) {
     int k;
     double pct;
     quiet_count(T, prm, &k, &pct);
     const int n2_all = next_pow2(T), n2_sel = next_pow2(k);
-    hipLaunchKernelGGL(frame_energy_kernel, dim3((T + 3) / 4, (unsigned)n_sig), dim3(256), 0, s, P,
-                       T, B, eps, w.energy);
     hipLaunchKernelGGL(select_quiet_kernel, dim3((unsigned)n_sig), dim3(1024),
                        (size_t)n2_all * 8 + 1024 * 4, s, (const double*)w.energy, T, n2_all, k,
                        w.sel);
@@ -602,6 +607,13 @@ static int launch_percentile(const double* P, const double* med, int64_t n_sig, 
                        eps, (double*)med, N, 0);
     CSE_CHECK_LAUNCH("noise percentile");
     return CSE_OK;
+}
+
+static int launch_percentile(const double* P, const double* med, int64_t n_sig, int T, int B,
+                             const cse_noise_params_t& prm, double eps, float* N, Workspace w,
+                             hipStream_t s) {
+    launch_energy(P, n_sig, T, B, eps, w, s);
+    return launch_percentile_sel(P, med, n_sig, T, B, prm, eps, N, w, s);
 }
 
 static int launch_min_tracking(const double* P, const double* med, int64_t n_sig, int T, int B,
@@ -733,6 +745,27 @@ extern "C" int cse_noise_percentile_med(const double* P, const double* med, int6
     prm.percentile = percentile;
     return launch_percentile(P, med, n_sig, T, B, prm, eps, N, carve(workspace, n_sig, T, B),
                              (hipStream_t)stream);
+}
+
+extern "C" int cse_noise_percentile_med2(const double* P, const double* med, int64_t n_sig,
+                                         int T, int B, double percentile_a, double percentile_b,
+                                         double eps, float* N_a, float* N_b, void* workspace,
+                                         cse_stream_t stream) {
+    CSE_NOISE_SHAPE_CHECKS("cse_noise_percentile_med2");
+    CSE_CHECK_ARG(med && N_a && workspace, "cse_noise_percentile_med2: NULL pointer");
+    CSE_CHECK_ARG(T >= 5, "cse_noise_percentile_med2: T=%d < 5 (use the simple estimate)", T);
+    int rc = reserve_lds();
+    if (rc) return rc;
+    const Workspace w = carve(workspace, n_sig, T, B);
+    const hipStream_t s = (hipStream_t)stream;
+    cse_noise_params_t prm;
+    cse_noise_default_params(&prm);
+    launch_energy(P, n_sig, T, B, eps, w, s);  // depends on eps only
+    prm.percentile = percentile_a;
+    rc = launch_percentile_sel(P, med, n_sig, T, B, prm, eps, N_a, w, s);
+    if (rc || !N_b) return rc;
+    prm.percentile = percentile_b;
+    return launch_percentile_sel(P, med, n_sig, T, B, prm, eps, N_b, w, s);
 }
 
 extern "C" int cse_noise_min_tracking_med(const double* P, const double* med, int64_t n_sig,

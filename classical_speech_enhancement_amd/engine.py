@@ -438,12 +438,23 @@ class GridPlan:
                     _ptr(P), _ptr(self.med), S, T, B, float(a_[3]), _ptr(raw(a_)),
                     float(b_[3]) if b_ else 0.0, _ptr(raw(b_)) if b_ else None, _ptr(self.ws),
                     st), "cse_noise_min_tracking_med")
+            # percentile estimates in pairs sharing eps: one frame-energy pass per pair
+            pc = {}
+            for b in bases:
+                if b[1] == "percentile":
+                    pc.setdefault(float(b[3]), []).append(b)
+            for eps, group in pc.items():
+                for k in range(0, len(group), 2):
+                    a_, b_ = group[k], (group[k + 1] if k + 1 < len(group) else None)
+                    _lib.check(lib.cse_noise_percentile_med2(
+                        _ptr(P), _ptr(self.med), S, T, B, float(a_[2]),
+                        float(b_[2]) if b_ else 0.0, eps, _ptr(raw(a_)),
+                        _ptr(raw(b_)) if b_ else None, _ptr(self.ws), st),
+                        "cse_noise_percentile_med2")
             for b in bases:
                 _, method, pct, eps = b
                 if method == "percentile":
-                    _lib.check(lib.cse_noise_percentile_med(
-                        _ptr(P), _ptr(self.med), S, T, B, float(pct), float(eps), _ptr(raw(b)),
-                        _ptr(self.ws), st), "cse_noise_percentile_med")
+                    continue
                 elif method == "simple":
                     _lib.check(lib.cse_noise_estimate(0, _ptr(P), S, T, B, 25.0, float(eps),
                                                       _ptr(raw(b)), _ptr(self.ws), st),

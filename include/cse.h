@@ -187,6 +187,14 @@ int cse_noise_median(const double* P, int64_t n_sig, int T, int B, double* med,
 int cse_noise_percentile_med(const double* P, const double* med, int64_t n_sig, int T, int B,
                              double percentile, double eps, float* N, void* workspace,
                              cse_stream_t stream);
+/* Two percentile estimates with one eps (pct 10 and 20 of the grids,
+ * parameter_ranges.py): the frame energies e_t = mean_b log(max(P, eps))
+ * (noise_estimation.py:44) depend on eps only and are computed once; each
+ * percentile then selects its quiet frames and takes its statistic as
+ * cse_noise_percentile_med does.  N_b may be NULL. */
+int cse_noise_percentile_med2(const double* P, const double* med, int64_t n_sig, int T, int B,
+                              double percentile_a, double percentile_b, double eps, float* N_a,
+                              float* N_b, void* workspace, cse_stream_t stream);
 int cse_noise_min_tracking_med(const double* P, const double* med, int64_t n_sig, int T, int B,
                                double eps, float* N, double eps_b, float* N_b, void* workspace,
                                cse_stream_t stream);
