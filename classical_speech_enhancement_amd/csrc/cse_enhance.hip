@@ -107,9 +107,10 @@ __device__ __forceinline__ float mmse_bracket(float v, float sqrtv) {
 // (MMSE, OMLSA); with rr = 0 and alpha_t = 0 on frame 0 the general DD
 // expression alpha_t*rr + (1-alpha_t)*d gives exactly that (for ksi_min >= 0),
 // so there is no per-bin branch to split the scheduling region.
-__device__ __forceinline__ float gain_wiener(float gam, float d, float& rr, float alpha_t,
+// dd = (1 - alpha_t) d, the ML term's share (gain_bin forms it with the per-bin row)
+__device__ __forceinline__ float gain_wiener(float gam, float dd, float& rr, float alpha_t,
                                              float gfloor) {
-    const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * d, 1e-10f);
+    const float xi = fmaxf(fmaf(alpha_t, rr, dd), 1e-10f);
     // np.clip as one v_med3; gfloor arrives as min(gain_floor, 1), numpy's
     // result when the bounds cross
     const float g = __builtin_amdgcn_fmed3f(xi * fast_rcp(1.0f + xi), gfloor, 1.0f);
@@ -118,9 +119,9 @@ __device__ __forceinline__ float gain_wiener(float gam, float d, float& rr, floa
 }
 
 // cig = (sqrt(pi)/2) / (gamma + 1e-12), per bin from the row stager
-__device__ __forceinline__ float gain_mmse(float gam, float d, float cig, float& rr, float alpha_t,
+__device__ __forceinline__ float gain_mmse(float gam, float dd, float cig, float& rr, float alpha_t,
                                            float ksi_min, float gmin, float gmax) {
-    const float xi = fmaxf(alpha_t * rr + (1.0f - alpha_t) * d, ksi_min);
+    const float xi = fmaxf(fmaf(alpha_t, rr, dd), ksi_min);
     const float v = __builtin_amdgcn_fmed3f(xi * gam * fast_rcp(1.0f + xi), 1e-12f, 80.0f);
     const float sv = __builtin_amdgcn_sqrtf(v);
     const float h = mmse_bracket(v, sv);
@@ -147,7 +148,7 @@ __device__ __forceinline__ float gain_mmse(float gam, float d, float cig, float&
 //   degree-11 polynomial took 12).  Dn lies in [0.045, 1] and A <= e^80, so
 //   neither (A + 1 - q) Dn nor A ((L - lgf) Dn + Pn) overflows.
 // The bin works on v' = v log2(e), the exp2 argument of Lambda: gam2 = gamma
-// log2(e) (the n_fft 512 stager stores it so), the decision-directed state
+// log2(e) (the stager stores it so at both n_fft), the decision-directed state
 // rr = G^2 gam2 (so its weight is alpha ln 2), the rational in v' and
 // L' = log2(xr rsq(v')) = L - 0.5 log2(log2 e), the constant folded into lgf_c.
 constexpr float kLn2 = 0.69314718055994531f;
@@ -157,10 +158,10 @@ constexpr float kLsaC = 0.26438318647244886f;  // 0.5 log2(log2 e)
 // gives g = exp2(-inf) = 0 -> clip -> gain_floor, the reference's 0**p * gf**(1-p)
 // clipped (p >= 1e-10 > 0).  Non-finite input makes the cell non-finite either way.
 // gclip = min(gain_floor, 1): the lower bound of the final np.clip
-__device__ __forceinline__ float gain_omlsa(float gam2, float d, float& rr, float a_rr, float a_d,
+__device__ __forceinline__ float gain_omlsa(float gam2, float dd, float& rr, float a_rr,
                                             float ksi_min, float gclip, float lg2_floor,
                                             float lgf_c, float q, float vmax2) {
-    const float xi = fmaxf(a_rr * rr + a_d * d, ksi_min);
+    const float xi = fmaxf(fmaf(a_rr, rr, dd), ksi_min);
     const float r = fast_rcp(1.0f + xi);
     const float xr = xi * r;
     const float v2 = __builtin_amdgcn_fmed3f(xr * gam2, 1e-12f * kLog2e, vmax2);
@@ -301,7 +302,7 @@ struct CellParam {
 static_assert(sizeof(CellParam) == 32, "CellParam layout");
 
 // One bin's shared row values (staged once per workgroup and frame):
-//   Wiener/MMSE/OMLSA: g = gamma (OMLSA at 512: gamma log2(e)), d = max(gamma - 1, 0) (512; 1024 computes d
+//   Wiener/MMSE/OMLSA: g = gamma (OMLSA: gamma log2(e)), d = max(gamma - 1, 0) (512; 1024 computes d
 //     here), a = (sqrt(pi)/2)/(gamma + 1e-12) (MMSE at 512);
 //   SS at 512: g = N, d = P = |Y|^2, a = 1/|Y| (gain output only), and the Y
 //     row holds the unit phasor of Y instead of Y ((1, 0) where Y = 0);
@@ -342,16 +343,20 @@ __device__ __forceinline__ float gain_bin(float2& y, RowV rv, float& rr, float a
         y = (pz > 0.0f) ? make_float2(yx, yy) : make_float2(1.0f, 0.0f);  // angle(0) = 0
         return (pz > 0.0f) ? u : sp;
     }
-    const float d = R2 ? rv.d : fmaxf(rv.g - 1.0f, 0.0f);
+    // dd = (1 - alpha_t) max(gamma - 1, 0): at 512 d is the stager's row; at 1024
+    // max((1 - alpha_t) gamma - (1 - alpha_t), 0), one FMA and a max (OMLSA's row
+    // holds gamma log2(e) at both n_fft, so its FMA takes (1 - alpha_t) ln 2).
+    // The per-frame weights are common to the bins (hoisted).
+    const float a_d = 1.0f - alpha_t;
+    const float dd = R2 ? a_d * rv.d
+                        : fmaxf(fmaf(rv.g, ALGO == CSE_ALGO_OMLSA ? a_d * kLn2 : a_d, -a_d), 0.0f);
     if (ALGO == CSE_ALGO_WIENER) {
-        g = gain_wiener(rv.g, d, rr, alpha_t, cp.p1);
+        g = gain_wiener(rv.g, dd, rr, alpha_t, cp.p1);
     } else if (ALGO == CSE_ALGO_MMSE) {
         const float cig = R2 ? rv.a : 0.88622692545275801f * fast_rcp(rv.g + 1e-12f);
-        g = gain_mmse(rv.g, d, cig, rr, alpha_t, cp.p1, cp.p2, cp.p3);
+        g = gain_mmse(rv.g, dd, cig, rr, alpha_t, cp.p1, cp.p2, cp.p3);
     } else {
-        // per-frame terms (alpha_t ln 2, 1 - alpha_t, ...) are common to the bins
-        const float gam2 = R2 ? rv.g : rv.g * kLog2e;
-        g = gain_omlsa(gam2, d, rr, alpha_t * kLn2, 1.0f - alpha_t, cp.p1, cp.gclip, cp.lg2_floor,
+        g = gain_omlsa(rv.g, dd, rr, alpha_t * kLn2, cp.p1, cp.gclip, cp.lg2_floor,
                        cp.lg2_floor - kLsaC, cp.q_spp, cp.p4 * kLog2e);
     }
     return g;
@@ -630,7 +635,8 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     const float P = y.x * y.x + y.y * y.y;
                     if (!W::R2) {
                         yrow[k] = y;
-                        grow[k] = (ALGO == CSE_ALGO_SS) ? pn[u] : fmaxf(P * pn[u], EPS);
+                        const float gam = fmaxf(P * pn[u], EPS);
+                        grow[k] = (ALGO == CSE_ALGO_SS) ? pn[u] : (ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam);
                     } else if (ALGO == CSE_ALGO_SS) {
                         // phasor y/|y| of the y rescaled by 2^64 below 2^-50
                         // (v_rsq flushes denormals); (1, 0) where y = 0

@@ -591,15 +591,10 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                 }
             }
             fdft16<true>(v);                           // v[k1] = A[n1][k1] (v[8..15] = 0)
-            {
-                const cd w = L.tw256[n1];
-                cd wr = w;
+            // twiddles e^{-2πi n1 k1/256} from the table (n1 k1 <= 225): 15
+            // independent reads instead of a 14-deep chain of fp64 complex products
 #pragma unroll
-                for (int k1 = 1; k1 < 16; ++k1) {
-                    v[k1] = dmul(v[k1], wr);
-                    wr = dmul(wr, w);
-                }
-            }
+            for (int k1 = 1; k1 < 16; ++k1) v[k1] = dmul(v[k1], L.tw256[n1 * k1]);
             // the transposes stay inside the frame's 16 lanes (one wave): after
             // the one workgroup barrier (t aliases e10), wave-level ordering
             double* t = L.u.t[fl];
@@ -621,18 +616,22 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
             wave_sync();                               // t reads issued before |X|^2 overwrites them
             // partner Z[(256 - k) mod 256]: lane (16 - k1) & 15, register 15 - k2 (k1 > 0)
             const int src = (tid & 48) | ((16 - k1) & 15);  // lane within the wave
-            double* pw = L.u.t[fl];  // |X|^2 of the frame, bins < 224, in its own rows
+            double* pw = L.u.t[fl];  // 4 |X|^2 of the frame, bins < 224, in its own rows
 #pragma unroll
-            for (int k2 = 0; k2 < 16; ++k2) {
+            for (int k2 = 0; k2 < 14; ++k2) {  // k < 224 (the bands end at bin 219)
                 const cd zo = v[15 - k2];
                 cd zp = dmk(__shfl(zo.x, src), __shfl(zo.y, src));
                 if (k1 == 0) zp = v[(16 - k2) & 15];
                 const cd z = v[k2];
-                const cd e = dmk(0.5 * (z.x + zp.x), 0.5 * (z.y - zp.y));
-                const cd od = dmk(0.5 * (z.y + zp.y), -0.5 * (z.x - zp.x));
-                const int k = k1 + 16 * k2;
-                const cd x = dadd(e, dmul(L.tw512[k], od));  // X[k] = E + e^{-2πi k/512} O
-                if (k < 224) pw[k] = fma(x.x, x.x, x.y * x.y);
+                // 2X[k] = 2E + e^{-2πi k/512} 2O, 2E = z + conj(zp), 2O = -i (z - conj(zp)):
+                // the halves are left out (exact power-of-two scalings) and the
+                // band sums take 1/4 (sqrt(s/4) = sqrt(s)/2 exactly)
+                const double ex = z.x + zp.x, ey = z.y - zp.y;
+                const double ox = z.y + zp.y, oy = zp.x - z.x;
+                const cd w = L.tw512[k1 + 16 * k2];
+                const double xr = fma(w.x, ox, fma(-w.y, oy, ex));
+                const double xi = fma(w.x, oy, fma(w.y, ox, ey));
+                pw[k1 + 16 * k2] = fma(xr, xr, xi * xi);
             }
             // ---- band envelopes of the frame by its own 16 lanes (one wave:
             // no workgroup barrier; the next block's first barrier protects pw)
@@ -640,7 +639,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
             if (n1 < NBAND && fl < nf) {
                 double s = 0.0;
                 for (int k = BAND_EDGE[n1]; k < BAND_EDGE[n1 + 1]; ++k) s += pw[k];
-                env[(int64_t)(j0 + fl) * 16 + n1] = sqrt(s);
+                env[(int64_t)(j0 + fl) * 16 + n1] = 0.5 * sqrt(s);
             }
         }
     }
