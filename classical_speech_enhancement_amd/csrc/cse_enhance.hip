@@ -240,25 +240,27 @@ struct WG {
     // n_fft 1024 keeps two tables small.  The window keeps slots q < 16, since
     // slot q + 16 is n + N/2 and w(n + N/2) = 1 - w(n) (the full 32-slot table
     // fits the LDS budget once the twiddles shrink, but measured 64.9 vs
-    // 57.4 ms at 13 pairs).  The pass-1 twiddles come from two rotors per
-    // lane, e^{2πi i/M} and e^{2πi 4i/M} (16 B): tw_b = r1^(b mod 4) r4^(b div 4),
-    // 13 complex products, at most three roundings deep.  That replaced a
-    // 16-column table (keyed by b2, times W32^{h2 b} and a select on the other
-    // half of the lanes): -35 VALU and 7 of 8 LDS reads per frame, 58.2 ->
-    // 57.4 ms at 13 pairs.  n_fft 512 reads the full table (8 ds_read_b128).
+    // 57.4 ms at 13 pairs).  The pass-1 twiddles are products of powers of
+    // the lane's rotor r = e^{2πi i/M}: tw_b = r^(b mod 4) r^(4 (b div 4)), 9
+    // complex products, from a per-lane row of r, r^2, r^3, r^4, r^8, r^12
+    // (48 B; r02's two-rotor form, 16 B, squared and cubed them per frame: 4
+    // products more).  The rotors replaced a 16-column table (keyed by b2,
+    // times W32^{h2 b} and a select on the other half of the lanes): -35 VALU
+    // and 7 of 8 LDS reads per frame, 58.2 -> 57.4 ms at 13 pairs.  n_fft 512
+    // reads the full table (8 ds_read_b128).
     static constexpr bool HALF_TABLES = (NFFT == 1024);
     static constexpr bool ROTOR_TW = (NFFT == 1024);
     static constexpr int TWL = G::L;                              // twiddle columns (table form)
     // pass-1 twiddles (512): one row of 18 complex (144 B) per column, entry
     // b - 1: the ds_read_b128 of a 16-lane group hit disjoint banks;
-    // (1024): cf[L][2] rotors
+    // (1024): cf[L][6] rotor powers
     static constexpr int OFF_TW = OFF_C + CBUF;
     // packing rotors e^{2πi (i + L j)/NFFT}: a row of the 8 (j < 8) per lane,
     // stride 80 B (20 dwords: the ds_read_b128 of a 16-lane group hit
     // disjoint banks), 4 ds_read_b128 per frame instead of 7 complex products
     static constexpr bool ROT_TABLE = R2 || CSE_ROT_TABLE_1024;
     static constexpr int ROTSTR = 80;
-    static constexpr int OFF_LC = OFF_TW + (ROTOR_TW ? G::L * 16 : TWL * 144);
+    static constexpr int OFF_LC = OFF_TW + (ROTOR_TW ? G::L * 48 : TWL * 144);
     static constexpr int OFF_CP = OFF_LC + G::L * (ROT_TABLE ? ROTSTR : 8);  // CellParam[CPWG]
     // synthesis window w(n)/(NFFT wss(n)) at the lane's 32 (16) sample slots,
     // wss the steady-state window-square sum of this workgroup's hop (librosa's
@@ -531,10 +533,13 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     // ---- workgroup tables: pass-1 twiddles e^{2πi i b/M} [b-1][i], lane
     // constants [i], cell parameters [slot]
     if constexpr (W::ROTOR_TW) {
-        for (int e = tid; e < 2 * L; e += W::THREADS) {
-            const int ii = e >> 1, b = (e & 1) ? 4 : 1;
+        // per lane r^p, p = 1, 2, 3, 4, 8, 12 (r = e^{2πi ii/M}): a 48-B row, the
+        // ds_read_b128 of a 16-lane group on disjoint banks (stride 12 dwords)
+        for (int e = tid; e < 6 * L; e += W::THREADS) {
+            const int ii = e / 6, k = e - 6 * (e / 6);
+            const int pw = k < 3 ? k + 1 : 4 * (k - 2);
             double s, c;
-            sincospi(2.0 * (double)(ii * b) / (double)M, &s, &c);
+            sincospi(2.0 * (double)(ii * pw) / (double)M, &s, &c);
             ((cf*)(smem + W::OFF_TW))[e] = cmk((float)c, (float)s);
         }
     } else {
@@ -749,14 +754,14 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             CSE_MARK("pass1");
             {
                 if constexpr (W::ROTOR_TW) {
-                    // twiddles e^{2πi i b/M} = r1^(b mod 4) r4^(b div 4) from the lane's
-                    // two rotors (one ds_read_b128; at most 3 roundings deep)
-                    const float4 q4 = *(const float4*)(smem + W::OFF_TW + 16 * i);
-                    const cf r1 = cmk(q4.x, q4.y), r4 = cmk(q4.z, q4.w);
+                    // twiddles e^{2πi i b/M} = r^(b mod 4) r^(4 (b div 4)) from the
+                    // lane's table of r, r^2, r^3, r^4, r^8, r^12 (three ds_read_b128;
+                    // one rounding per table entry, one product at most)
+                    const float4* q4 = (const float4*)(smem + W::OFF_TW + 48 * i);
+                    const float4 qa = q4[0], qb = q4[1], qc = q4[2];
                     idft16(z);
-                    const cf r2 = cmul(r1, r1), r8 = cmul(r4, r4);
-                    const cf lo[4] = {cmk(1.0f, 0.0f), r1, r2, cmul(r2, r1)};
-                    const cf hi[4] = {cmk(1.0f, 0.0f), r4, r8, cmul(r8, r4)};
+                    const cf lo[4] = {cmk(1.0f, 0.0f), cmk(qa.x, qa.y), cmk(qa.z, qa.w), cmk(qb.x, qb.y)};
+                    const cf hi[4] = {cmk(1.0f, 0.0f), cmk(qb.z, qb.w), cmk(qc.x, qc.y), cmk(qc.z, qc.w)};
 #pragma unroll
                     for (int b = 1; b < 16; ++b) {
                         const cf t = (b & 3) == 0 ? hi[b >> 2] : (b < 4 ? lo[b] : cmul(lo[b & 3], hi[b >> 2]));
