@@ -13,7 +13,6 @@ the reference plugin's keyword arguments (parameter_ranges.py keys).
 """
 
 import ctypes
-import os
 import math
 from collections import OrderedDict
 
@@ -56,21 +55,6 @@ def _ptr(t):
 
 def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-
-
-_AUX = {}
-
-
-def _aux_streams(device, n):
-    """n auxiliary streams of this device, created once per process (HIP maps
-    streams onto a small pool of hardware queues: a fixed set avoids creating
-    one per plan)."""
-    if n <= 0:
-        return []
-    lst = _AUX.setdefault(str(device), [])
-    while len(lst) < n:
-        lst.append(torch.cuda.Stream(device=device))
-    return lst[:n]
 
 
 def n_frames(length, hop):
@@ -337,8 +321,8 @@ class GridPlan:
                 self.raw_off[base] = (roff, 1 if src_static else T)
                 roff += S * (B if src_static else T * B)
             r0, src_frames = self.raw_off[base]
-            jobs.append((hop, (r0, noff, src_frames, 1 if static else T, float(mu or 0.0),
-                               float(eps) if inverse else 0.0)))
+            jobs.append((r0, noff, src_frames, 1 if static else T, float(mu or 0.0),
+                         float(eps) if inverse else 0.0))
             noff += S * per_sig
             if method == "true_noise" and hop not in self.Ptrue:
                 if not with_clean:
@@ -347,19 +331,15 @@ class GridPlan:
                                               dtype=torch.float64, device=dev)
         self.pool = torch.empty(noff, dtype=torch.float32, device=dev)
         self.raw = torch.empty(max(roff, 1), dtype=torch.float32, device=dev)
-        # per hop: its cse_noise_finish jobs, median row and workspace, so the
-        # hops' analysis chains can run side by side (prepare)
+        jt = np.zeros(len(jobs), dtype=_lib.NOISE_JOB_DTYPE)
+        for j, (so, do, sf, of, mu, ie) in enumerate(jobs):
+            jt[j] = (so, do, sf, of, mu, ie)
         self.n_jobs = len(jobs)
-        self.jobs_h, self.med_h, self.ws_h = {}, {}, {}
-        for h in self.hops:
-            js = [j for (hh, j) in jobs if hh == h]
-            jt = np.zeros(len(js), dtype=_lib.NOISE_JOB_DTYPE)
-            for j, (so, do, sf, of, mu, ie) in enumerate(js):
-                jt[j] = (so, do, sf, of, mu, ie)
-            self.jobs_h[h] = (torch.from_numpy(jt.view(np.uint8).copy()).to(dev), len(js))
-            self.med_h[h] = torch.empty((S, B), dtype=torch.float64, device=dev)
-            self.ws_h[h] = torch.empty(int(eng.lib.cse_noise_workspace_bytes(S, n_frames(L, h), B)),
-                                       dtype=torch.uint8, device=dev)
+        self.jobs_d = torch.from_numpy(jt.view(np.uint8).copy()).to(dev)
+        self.med = torch.empty((S, B), dtype=torch.float64, device=dev)
+        Tmax = max(n_frames(L, h) for h in self.hops)
+        self.ws = torch.empty(int(eng.lib.cse_noise_workspace_bytes(S, Tmax, B)),
+                              dtype=torch.uint8, device=dev)
         # ---- cell table (columns gathered once, written as arrays)
         n = len(items)
         cells = np.zeros(n, dtype=_lib.CELL_DTYPE)
@@ -426,93 +406,68 @@ class GridPlan:
             self.xst_d = torch.zeros(len(items), dtype=torch.int32, device=dev)
 
     def prepare(self, noisy, clean=None):
-        """Group-level analysis: STFTs and every noise row (once per signal batch).
-
-        The hops' chains (STFT, median, min-tracking and percentile passes, the
-        finish jobs of that hop's noise keys) share nothing, so the second hop
-        runs on an auxiliary stream forked from and joined back into the
-        current one: after an enhance launch, which holds every CU, the two
-        chains of short dependent kernels overlap instead of queueing."""
-        st0 = torch.cuda.current_stream()
-        serial = os.environ.get("CSE_SERIAL_HOPS") == "1"  # A/B switch: one stream
-        aux = [] if serial else _aux_streams(self.device, len(self.hops) - 1)
-        if aux:
-            ev = torch.cuda.Event()
-            ev.record(st0)
-            for s_ in aux:
-                s_.wait_event(ev)
-        for hop, s_ in zip(self.hops, [st0] + aux):
-            with torch.cuda.stream(s_):
-                self._prepare_hop(hop, noisy, clean)
-        for s_ in aux:
-            ev = torch.cuda.Event()
-            ev.record(s_)
-            st0.wait_event(ev)
-        self.clean = clean if self.with_clean else None
-
-    def _prepare_hop(self, hop, noisy, clean):
+        """Group-level analysis: STFTs and every noise row (once per signal batch)."""
         S, L, B = self.S, self.L, self.B
         lib = self.lib
         st = _stream()
-        med, ws = self.med_h[hop], self.ws_h[hop]
-        T = n_frames(L, hop)
-        yv = self.Ybuf[2 * self.y_base[hop]:2 * (self.y_base[hop] + S * T * B)]
-        _lib.check(lib.cse_stft(_ptr(noisy), None, S, L, self.n_fft, hop, _ptr(yv),
-                                _ptr(self.P[hop]), st), "cse_stft")
-        if hop in self.Ptrue:
-            m = self.true_len
-            xn, xc = noisy, clean
-            if m < L:  # the STFT of the trimmed difference (noise_estimation.py:128-133)
-                xn, xc = noisy[:, :m].contiguous(), clean[:, :m].contiguous()
-            _lib.check(lib.cse_stft(_ptr(xn), _ptr(xc), S, m, self.n_fft, hop, None,
-                                    _ptr(self.Ptrue[hop]), st), "cse_stft(true)")
-        bases = [b for b in self.raw_off if b[0] == hop]
-        P = self.P[hop]
+        for hop in self.hops:
+            T = n_frames(L, hop)
+            yv = self.Ybuf[2 * self.y_base[hop]:2 * (self.y_base[hop] + S * T * B)]
+            _lib.check(lib.cse_stft(_ptr(noisy), None, S, L, self.n_fft, hop, _ptr(yv),
+                                    _ptr(self.P[hop]), st), "cse_stft")
+            if hop in self.Ptrue:
+                m = self.true_len
+                xn, xc = noisy, clean
+                if m < L:  # the STFT of the trimmed difference (noise_estimation.py:128-133)
+                    xn, xc = noisy[:, :m].contiguous(), clean[:, :m].contiguous()
+                _lib.check(lib.cse_stft(_ptr(xn), _ptr(xc), S, m, self.n_fft, hop, None,
+                                        _ptr(self.Ptrue[hop]), st), "cse_stft(true)")
+            bases = [b for b in self.raw_off if b[0] == hop]
+            P = self.P[hop]
 
-        def raw(b):
-            o, frames = self.raw_off[b]
-            return self.raw[o:o + S * frames * B]
-        if T >= 5 and any(m in ("percentile", "min_tracking") for (_, m, _, _) in bases):
-            _lib.check(lib.cse_noise_median(_ptr(P), S, T, B, _ptr(med), st),
-                       "cse_noise_median")
-        mt = [b for b in bases if b[1] == "min_tracking"]
-        for k in range(0, len(mt), 2):  # two eps per IIR + min-filter pass
-            a_, b_ = mt[k], (mt[k + 1] if k + 1 < len(mt) else None)
-            _lib.check(lib.cse_noise_min_tracking_med(
-                _ptr(P), _ptr(med), S, T, B, float(a_[3]), _ptr(raw(a_)),
-                float(b_[3]) if b_ else 0.0, _ptr(raw(b_)) if b_ else None, _ptr(ws),
-                st), "cse_noise_min_tracking_med")
-        # percentile estimates in pairs sharing eps: one frame-energy pass per pair
-        pc = {}
-        for b in bases:
-            if b[1] == "percentile":
-                pc.setdefault(float(b[3]), []).append(b)
-        for eps, group in pc.items():
-            for k in range(0, len(group), 2):
-                a_, b_ = group[k], (group[k + 1] if k + 1 < len(group) else None)
-                _lib.check(lib.cse_noise_percentile_med2(
-                    _ptr(P), _ptr(med), S, T, B, float(a_[2]),
-                    float(b_[2]) if b_ else 0.0, eps, _ptr(raw(a_)),
-                    _ptr(raw(b_)) if b_ else None, _ptr(ws), st),
-                    "cse_noise_percentile_med2")
-        for b in bases:
-            _, method, pct, eps = b
-            if method == "percentile":
-                continue
-            elif method == "simple":
-                _lib.check(lib.cse_noise_estimate(0, _ptr(P), S, T, B, 25.0, float(eps),
-                                                  _ptr(raw(b)), _ptr(ws), st),
-                           "cse_noise_estimate(simple)")
-            elif method == "true_noise":
-                prm = noise_params(src_frames=self.Ptrue[hop].shape[1])
-                _lib.check(lib.cse_noise_estimate_ex(2, _ptr(self.Ptrue[hop]), S, T, B,
-                                                     ctypes.byref(prm), float(eps),
-                                                     _ptr(raw(b)), None, st),
-                           "cse_noise_estimate(true)")
-        jobs_d, n_jobs = self.jobs_h[hop]
-        if n_jobs:
-            _lib.check(lib.cse_noise_finish(_ptr(jobs_d), n_jobs, S, B, _ptr(self.raw),
-                                            _ptr(self.pool), st), "cse_noise_finish")
+            def raw(b):
+                o, frames = self.raw_off[b]
+                return self.raw[o:o + S * frames * B]
+            if T >= 5 and any(m in ("percentile", "min_tracking") for (_, m, _, _) in bases):
+                _lib.check(lib.cse_noise_median(_ptr(P), S, T, B, _ptr(self.med), st),
+                           "cse_noise_median")
+            mt = [b for b in bases if b[1] == "min_tracking"]
+            for k in range(0, len(mt), 2):  # two eps per IIR + min-filter pass
+                a_, b_ = mt[k], (mt[k + 1] if k + 1 < len(mt) else None)
+                _lib.check(lib.cse_noise_min_tracking_med(
+                    _ptr(P), _ptr(self.med), S, T, B, float(a_[3]), _ptr(raw(a_)),
+                    float(b_[3]) if b_ else 0.0, _ptr(raw(b_)) if b_ else None, _ptr(self.ws),
+                    st), "cse_noise_min_tracking_med")
+            # percentile estimates in pairs sharing eps: one frame-energy pass per pair
+            pc = {}
+            for b in bases:
+                if b[1] == "percentile":
+                    pc.setdefault(float(b[3]), []).append(b)
+            for eps, group in pc.items():
+                for k in range(0, len(group), 2):
+                    a_, b_ = group[k], (group[k + 1] if k + 1 < len(group) else None)
+                    _lib.check(lib.cse_noise_percentile_med2(
+                        _ptr(P), _ptr(self.med), S, T, B, float(a_[2]),
+                        float(b_[2]) if b_ else 0.0, eps, _ptr(raw(a_)),
+                        _ptr(raw(b_)) if b_ else None, _ptr(self.ws), st),
+                        "cse_noise_percentile_med2")
+            for b in bases:
+                _, method, pct, eps = b
+                if method == "percentile":
+                    continue
+                elif method == "simple":
+                    _lib.check(lib.cse_noise_estimate(0, _ptr(P), S, T, B, 25.0, float(eps),
+                                                      _ptr(raw(b)), _ptr(self.ws), st),
+                               "cse_noise_estimate(simple)")
+                elif method == "true_noise":
+                    prm = noise_params(src_frames=self.Ptrue[hop].shape[1])
+                    _lib.check(lib.cse_noise_estimate_ex(2, _ptr(self.Ptrue[hop]), S, T, B,
+                                                         ctypes.byref(prm), float(eps),
+                                                         _ptr(raw(b)), None, st),
+                               "cse_noise_estimate(true)")
+        _lib.check(lib.cse_noise_finish(_ptr(self.jobs_d), self.n_jobs, S, B, _ptr(self.raw),
+                                        _ptr(self.pool), st), "cse_noise_finish")
+        self.clean = clean if self.with_clean else None
 
     def enhance(self):
         """THE HOT PATH launch: every cell of this n_fft, one kernel."""
