@@ -435,6 +435,8 @@ def main():
     ap.add_argument("--no-sweep", action="store_true",
                     help="skip the sweep block (search.run_grid with alignment and STOI)")
     args = ap.parse_args()
+    if args.pipeline < 1:
+        ap.error("--pipeline must be >= 1")
 
     import torch
     import torch.distributed as dist
