@@ -55,6 +55,8 @@ def main():
         times.append(e0.elapsed_time(e1))
     ms = float(np.median(times))
     v = out.cpu().numpy()
+    if os.environ.get("CSE_STOI_DUMP"):  # per-cell scores, to compare resampler paths
+        np.save(os.environ["CSE_STOI_DUMP"], v)
     if not os.environ.get("CSE_BENCH_NOCHECK"):
         assert os.environ.get("CSE_BENCH_NOCHECK") or np.isfinite(v).all()
     print(json.dumps({"what": "cse_stoi_cells", "cells": a.cells, "clip_s": a.seconds,
