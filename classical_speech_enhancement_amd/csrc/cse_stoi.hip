@@ -54,7 +54,7 @@ constexpr int CST = 128;                 // coefficient row stride
 constexpr int FR = 256, HOP = 128;       // frames at 10 kHz
 constexpr int NBAND = 15, NSEG = 30;
 constexpr int FB = 16;                   // most STFT frames per phase-A block
-constexpr int MAXD = 24;                 // most distinct 10-kHz half-blocks per block
+constexpr int MAXD = 28;                 // most distinct 10-kHz half-blocks per block
 // block table (ints): D, j0, nf, p[MAXD], sa[FB + 1], sb[FB + 1].  A block takes
 // frames while nf <= FB and its OLA rows need <= MAXD distinct half-blocks
 // (a row needs at most 2, so every block but the last has >= 13 frames)
@@ -86,9 +86,9 @@ static_assert(SSTR >= 8 * SROW && SSTR % 64 == GRP, "staging slot stride");
 constexpr int MF_ED = 5, MF_CD = 6, MF_KC = 3;
 constexpr int MF_PL = 384;                  // bytes per digit plane and slot (>= 24 * 8 + 192)
 constexpr int MF_SL = MF_ED * MF_PL;        // bytes per slot
-constexpr int MF_ROWS = SLOTS * 9;          // GEMM rows per chunk
+constexpr int MF_SLOTS = 7;                 // slots per chunk: 63 rows = 4 tiles, one per wave
 constexpr int MF_BTAB = MF_CD * MF_KC * 4 * 16 * 16;  // coefficient digit fragments (bytes)
-constexpr int STAGE_F = (MF_SL * SLOTS / 4 > SLOTS * SSTR) ? MF_SL * SLOTS / 4 : SLOTS * SSTR;
+constexpr int STAGE_F = (MF_SL * MF_SLOTS / 4 > SLOTS * SSTR) ? MF_SL * MF_SLOTS / 4 : SLOTS * SSTR;
 constexpr int NT = 256;                  // threads per workgroup
 constexpr double EPS = 2.220446049250313e-16; // np.finfo(float).eps
 __constant__ int BAND_EDGE[NBAND + 1] = {7, 9, 11, 14, 17, 22, 27, 34, 43, 55,
@@ -504,6 +504,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
     // Lane tid stages slot fs = tid / FW (FW = 28 lanes per slot, 9 slots), samples
     // uu = fr + FW u: one block-table read and one base index per fetch, the
     // loads at constant strides from it
+    constexpr int NSL = MF ? MF_SLOTS : SLOTS;            // slots per chunk
     constexpr int FW = 28, NU = 8 * GRP + KN;             // NU = 339 samples staged per slot
     constexpr int PF = (NU + FW - 1) / FW;                // 13 loads per lane
     static_assert(SLOTS * FW <= NT, "staging lanes");
@@ -521,7 +522,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
     auto fetch = [&](const int* tb, int c0) {
         // lanes past the 9 slots (and slots past the chunk) read a table entry
         // in range and are never staged
-        const int q0 = (HOP * tb[T_P + c0 + min(fs, SLOTS - 1)]) / UP;
+        const int q0 = (HOP * tb[T_P + c0 + min(fs, NSL - 1)]) / UP;
         fbase = 8 * q0 + KLO + fr - lag - lo;
 #pragma unroll
         for (int u = 0; u < PF; ++u)
@@ -548,8 +549,8 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                 L.u.a.e10[d][n] = x10[(int64_t)tb[T_P + d] * HOP + n];
             }
         } else {
-            for (int c0 = 0; c0 < D; c0 += SLOTS) {
-                const int ns = min(SLOTS, D - c0);
+            for (int c0 = 0; c0 < D; c0 += NSL) {
+                const int ns = min(NSL, D - c0);
                 // stage e[8 q0 - 58 + uu], uu < 339, at [uu & 7][uu >> 3] (MF:
                 // its 5 digits at byte uu of the slot's digit planes)
                 if (fs < ns) {
@@ -573,13 +574,13 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                     }
                 }
                 __syncthreads();  // stage (and the next block's table) visible
-                if (c0 + SLOTS < D)
-                    fetch(tb, c0 + SLOTS);
+                if (c0 + NSL < D)
+                    fetch(tb, c0 + NSL);
                 else if (blk + 1 < nblk)
                     fetch(tn, 0);
                 if (MF) {
                     // GEMM tiles of 16 rows (slot, a) over the chunk's ns * 9 rows,
-                    // one wave per tile (MF_ROWS = 81: 6 tiles, waves 0-1 take two)
+                    // one wave per tile (7 slots: 63 rows, 4 tiles)
                     const int wv = tid >> 6, ln = tid & 63;
                     const int nrows = ns * 9;
                     for (int tile = wv; tile * 16 < nrows; tile += NT / 64) {
