@@ -84,6 +84,10 @@ static_assert(SSTR >= 8 * SROW && SSTR % 64 == GRP, "staging slot stride");
 // columns (15 used); lane l holds k = 16 (l >> 4) + b of its row / column l & 15
 // (any k map shared by A and B is exact: tools/micro/mfma_i8_layout.hip).
 constexpr int MF_ED = 5, MF_CD = 6, MF_KC = 3;
+#ifndef CSE_STOI_MF_S
+#define CSE_STOI_MF_S 5  // digit pairs kept: i + j <= CSE_STOI_MF_S
+#endif
+constexpr int MF_S = CSE_STOI_MF_S;
 constexpr int MF_PL = 384;                  // bytes per digit plane and slot (>= 24 * 8 + 192)
 constexpr int MF_SL = MF_ED * MF_PL;        // bytes per slot
 constexpr int MF_SLOTS = 7;                 // slots per chunk: 63 rows = 4 tiles, one per wave
@@ -588,12 +592,12 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                         const int rw = row < nrows ? row : 0;  // rows past the chunk read slot 0
                         const signed char* ab = (const signed char*)L.u.a.stage + (rw / 9) * MF_SL +
                                                 24 * (rw % 9) + 16 * (ln >> 4);
-                        mf_i4 acc[MF_CD];
+                        mf_i4 acc[MF_S + 1];
 #pragma unroll
-                        for (int t = 0; t < MF_CD; ++t) acc[t] = mf_i4{0, 0, 0, 0};
+                        for (int t = 0; t <= MF_S; ++t) acc[t] = mf_i4{0, 0, 0, 0};
 #pragma unroll 1
                         for (int c = 0; c < MF_KC; ++c) {
-                            mf_i4 A[MF_ED], Bf[MF_CD];
+                            mf_i4 A[MF_ED], Bf[MF_S + 1];
 #pragma unroll
                             for (int i = 0; i < MF_ED; ++i) {
                                 const int2* a2 = (const int2*)(ab + i * MF_PL + 64 * c);
@@ -601,14 +605,14 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                                 A[i] = mf_i4{lo2.x, lo2.y, hi2.x, hi2.y};
                             }
 #pragma unroll
-                            for (int j = 0; j < MF_CD; ++j)
+                            for (int j = 0; j <= MF_S; ++j)
                                 Bf[j] = *(const mf_i4*)(coefq + (((j * MF_KC + c) * 4 + (ln >> 4)) * 16 +
                                                                  (ln & 15)) * 16);
 #pragma unroll
                             for (int i = 0; i < MF_ED; ++i)
 #pragma unroll
-                                for (int j = 0; j < MF_CD; ++j)
-                                    if (i + j < MF_CD)
+                                for (int j = 0; j <= MF_S; ++j)
+                                    if (i + j <= MF_S)
                                         acc[i + j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
                                             A[i], Bf[j], acc[i + j], 0, 0, 0);
                         }
@@ -623,7 +627,8 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                                     const int sl = crow / 9, a = crow - 9 * (crow / 9);
                                     double h = (double)acc[0][reg];
 #pragma unroll
-                                    for (int t = 1; t < MF_CD; ++t) h = fma(h, 256.0, (double)acc[t][reg]);
+                                    for (int t = 1; t <= MF_S; ++t) h = fma(h, 256.0, (double)acc[t][reg]);
+                                    h *= (double)(1ll << (8 * (5 - MF_S)));  // 256^(5 - S)
                                     const int p = tb[T_P + c0 + sl];
                                     const int q = (HOP * p) / UP + 3 * a + m;
                                     const int off = 5 * q + r - HOP * p;
