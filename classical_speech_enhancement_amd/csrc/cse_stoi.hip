@@ -85,7 +85,7 @@ static_assert(SSTR >= 8 * SROW && SSTR % 64 == GRP, "staging slot stride");
 // (any k map shared by A and B is exact: tools/micro/mfma_i8_layout.hip).
 constexpr int MF_ED = 5, MF_CD = 6, MF_KC = 3;
 #ifndef CSE_STOI_MF_S
-#define CSE_STOI_MF_S 5  // digit pairs kept: i + j <= CSE_STOI_MF_S
+#define CSE_STOI_MF_S 4  // digit pairs kept: i + j <= CSE_STOI_MF_S (4: 7e-11 of the fp64 FIR)
 #endif
 constexpr int MF_S = CSE_STOI_MF_S;
 constexpr int MF_PL = 384;                  // bytes per digit plane and slot (>= 24 * 8 + 192)
