@@ -69,12 +69,12 @@ from classical_speech_enhancement_amd.parameter_ranges import grid_specs  # noqa
 def _cpu_cell(args):
     """One reference cell on the CPU: (cell index, frames, lag-0 SNR of the
     clipped output, waveform as f64 or None)."""
-    idx, alg, params, seconds, want_y = args
+    idx, pair, alg, params, seconds, want_y = args
     import oracle
     from classical_speech_enhancement_amd.synth import make_pair
-    if getattr(_cpu_cell, "seconds", None) != seconds:
-        _cpu_cell.pair = make_pair(0, seconds)
-        _cpu_cell.seconds = seconds
+    if getattr(_cpu_cell, "key", None) != (pair, seconds):
+        _cpu_cell.pair = make_pair(pair, seconds)
+        _cpu_cell.key = (pair, seconds)
     clean, noisy = _cpu_cell.pair
     kw = dict(params)
     if kw["noise_method"] == "true_noise":
@@ -123,18 +123,19 @@ def parity_cells(seconds, n_fft, per_stratum=4, seed=7):
     return out
 
 
-def cpu_run(budget_s, seconds, n_fft, y_cells, timed=True):
+def cpu_run(budget_s, seconds, n_fft, y_cells, timed=True, pair=0):
     """Run the oracle on the host cores: first the y_cells (waveforms kept for
     the parity check), then (timed) cells drawn uniformly at random from the
-    pair-0 grid until budget_s of wall time.  Returns (baseline dict or None,
-    {cell: snr}, {cell: y})."""
+    pair's grid until budget_s of wall time.  Returns (baseline dict or None,
+    {cell: snr}, {cell: y}); cells are indices into grid_specs(1, n_fft)."""
     import multiprocessing as mp
     procs, aff, ncpu = _cpu_share()
     specs = grid_specs(1, n_fft)
     rng = np.random.default_rng(0)
     want = set(y_cells)
     order = [i for i in rng.permutation(len(specs)).tolist() if i not in want]
-    work = [(i, specs[i][1], specs[i][2], seconds, i in want) for i in list(y_cells) + order]
+    work = [(i, pair, specs[i][1], specs[i][2], seconds, i in want)
+            for i in list(y_cells) + order]
     env_keys = ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")
     saved = {k: os.environ.get(k) for k in env_keys}
     for k in env_keys:
@@ -145,7 +146,7 @@ def cpu_run(budget_s, seconds, n_fft, y_cells, timed=True):
     try:
         with mp.get_context("spawn").Pool(procs) as pool:
             # warm the workers (imports + synth) outside the window
-            list(pool.imap_unordered(_cpu_cell, [(0, w[1], w[2], seconds, False)
+            list(pool.imap_unordered(_cpu_cell, [(0, pair, w[2], w[3], seconds, False)
                                                  for w in work[:procs]]))
             stream = work if timed else work[:len(y_cells)]
             t0 = time.perf_counter()
@@ -254,6 +255,7 @@ class TimedJob:
         self.n_buf = n_buf
         self.mps = [eng.plan(S, L, specs, with_clean=True, align=align) for _ in range(n_buf)]
         self.units = self.mps[0].units
+        self.n_cells = len(specs)
         self.main_s = torch.cuda.current_stream()
         self.prep_s = torch.cuda.Stream() if n_buf > 1 else self.main_s
         self.ev_prep = [torch.cuda.Event() for _ in range(n_buf)]
@@ -291,6 +293,7 @@ class TimedJob:
             self.ev_copied = [None] * n_buf
         self.gathered = None
         self.gathered_buf = None
+        self.prep_evs = None
         for k in range(n_buf - 1):  # the analyses of the first n_buf - 1 steps
             self.prep(k)
 
@@ -300,8 +303,15 @@ class TimedJob:
         with torch.cuda.stream(self.prep_s):
             if self.ev_done[b] is not None:
                 self.prep_s.wait_event(self.ev_done[b])  # the enhance that last read these buffers
+            ev = None
+            if self.prep_evs is not None:  # timed region: the analysis chain's span
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(self.prep_s)
             for p in self.mps[b].plans:
                 p.prepare(self.noisy, self.clean)
+            if ev is not None:
+                ev[1].record(self.prep_s)
+                self.prep_evs.append(ev)
             self.ev_prep[b].record(self.prep_s)
 
     def step(self, evs=None):
@@ -372,7 +382,10 @@ class TimedJob:
 
     def run(self, steps, warmup):
         """Warmup, then K timed steps bracketed by barrier + synchronize; returns
-        (seconds, max over ranks; mean enhance-kernel ms per plan)."""
+        (seconds, max over ranks; mean enhance-kernel ms per plan).  Also sets
+        self.rank_stats: this rank's own figures (its wall seconds before the
+        max, the summed enhance-kernel ms per step, the analysis chain's span
+        per step on its side stream, units and pairs per step)."""
         torch = self.torch
         for _ in range(warmup):
             self.step()
@@ -380,6 +393,7 @@ class TimedJob:
         n_pl = len(self.mps[0].plans)
         evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 for _ in range(n_pl)] for _ in range(steps)]
+        self.prep_evs = []
         if self.dist is not None:
             self.dist.barrier()
         torch.cuda.synchronize()
@@ -387,6 +401,7 @@ class TimedJob:
         for k in range(steps):
             self.step(evs[k])
         torch.cuda.synchronize()
+        local = time.perf_counter() - t0
         if self.dist is not None:
             self.dist.barrier()
         dt = time.perf_counter() - t0
@@ -395,10 +410,47 @@ class TimedJob:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
             dt = float(t.item())
         kern = [float(np.mean([e[j][0].elapsed_time(e[j][1]) for e in evs])) for j in range(n_pl)]
+        ana = [s.elapsed_time(e) for s, e in self.prep_evs]
+        self.prep_evs = None
+        self.rank_stats = {"wall_s": local, "kernel_ms": float(sum(kern)),
+                           "analysis_ms": float(np.mean(ana)) if ana else 0.0,
+                           "units": float(self.units), "cells": float(self.n_cells)}
         return dt, kern
 
     def last_plans(self):
         return self.mps[(self.k - 1) % self.n_buf].plans
+
+
+RANK_FIELDS = ("wall_s", "kernel_ms", "analysis_ms", "units", "cells", "pairs")
+
+
+def gather_rank_stats(stats, dist_ctx):
+    """Every rank's own figures (TimedJob.rank_stats + its pair count) on every
+    rank, with the spread of the work over the ranks: max / mean of the
+    enhance-kernel time, of the rank's own wall time and of its units.  One
+    all_gather_into_tensor (RCCL on device tensors for backend nccl)."""
+    import torch
+    dist, coll_dev, world = dist_ctx
+    v = torch.tensor([float(stats[k]) for k in RANK_FIELDS], dtype=torch.float64)
+    if dist is not None:
+        out = torch.empty(world * len(RANK_FIELDS), dtype=torch.float64, device=coll_dev)
+        dist.all_gather_into_tensor(out, v.to(coll_dev))
+        v = out.cpu()
+    rows = v.numpy().reshape(-1, len(RANK_FIELDS))
+    ranks = [{k: (int(r[i]) if k in ("units", "cells", "pairs") else float(r[i]))
+              for i, k in enumerate(RANK_FIELDS)} for r in rows]
+
+    def spread(k):
+        x = rows[:, RANK_FIELDS.index(k)]
+        return float(x.max() / x.mean()) if x.mean() > 0 else None
+    return {"per_rank": ranks,
+            "imbalance_max_over_mean": {"kernel_ms": spread("kernel_ms"),
+                                        "wall_s": spread("wall_s"), "units": spread("units")},
+            "fields": ("wall_s: the rank's own timed seconds (before the max over ranks); "
+                       "kernel_ms: its enhance launch(es) per step, HIP events on the launch "
+                       "stream; analysis_ms: its STFT + noise-PSD chain per step, HIP events on "
+                       "the side stream it overlaps the enhance from; units, cells, pairs: its "
+                       "share of one step")}
 
 
 def main():
@@ -467,6 +519,7 @@ def main():
     units = job.units
     dt, kern = job.run(args.steps, args.warmup)
     kern_ms = kern[0]
+    ranks = gather_rank_stats(dict(job.rank_stats, pairs=len(pair_ids)), dist_ctx)
     n_cells_job = len(grid_specs(1, args.nfft)) * total_pairs
     table = job.table(n_cells_job)
     if args.dump_table and rank == 0:
@@ -510,6 +563,23 @@ def main():
     if not args.no_sweep:
         sweep = sweep_block(args, world, total_pairs, weak)
 
+    # ---- parity on every rank: the pair it holds most cells of, stratified
+    # cells' waveforms and the timed step's SNRs against the oracle; at N = 1
+    # the CPU baseline runs in the same pool (rank 0 only)
+    base, par = None, None
+    want_base = rank == 0 and world == 1 and not args.no_cpu_baseline
+    if not args.no_parity or want_base:
+        slot, held = rank_pair_cells(local_specs, args.nfft)
+        y_cells = [] if args.no_parity else pick_parity_cells(args.seconds, args.nfft, held)
+        base, cpu_snr, cpu_y = cpu_run(args.cpu_budget, args.seconds, args.nfft, y_cells,
+                                       timed=want_base, pair=pair_ids[slot])
+        if y_cells:
+            dev_snr = {g: float(snr_local[j]) for g, j in held.items()}
+            par = parity_block(eng, noisy[slot:slot + 1], clean[slot:slot + 1], clean_pow[slot],
+                               args.nfft, dev_snr, cpu_snr, cpu_y)
+            par["pair"] = int(pair_ids[slot])
+    par_all = gather_parity(par, dist_ctx) if not args.no_parity else None
+
     if rank != 0:
         if use_dist:
             dist.barrier()
@@ -547,23 +617,16 @@ def main():
             "finalize_alignment": bool(args.align),
         },
         "roofline": roofline_block(args.nfft, units, kern_ms),
+        "ranks": ranks,
     }
     if full is not None:
         res["full_grid"] = full
     if sweep is not None:
         res["sweep"] = sweep
-    if world == 1:
-        # pair 0 is the CPU's pair: its grid is this plan's first cells
-        y_cells = [] if args.no_parity else parity_cells(args.seconds, args.nfft)
-        base, cpu_snr, cpu_y = None, {}, {}
-        if not args.no_cpu_baseline or y_cells:
-            base, cpu_snr, cpu_y = cpu_run(args.cpu_budget, args.seconds, args.nfft, y_cells,
-                                           timed=not args.no_cpu_baseline)
-        if base:
-            res["cpu_baseline"] = base
-        if y_cells:
-            res["parity"] = parity_block(eng, noisy, clean, clean_pow, args.nfft, snr_local,
-                                         cpu_snr, cpu_y, weak)
+    if base:
+        res["cpu_baseline"] = base
+    if par_all is not None:
+        res["parity"] = dict(par or {}, **par_all)
     print(json.dumps(res))
     sys.stdout.flush()
     if use_dist:
@@ -580,17 +643,25 @@ def roofline_block(n_fft, units, kern_ms):
     binary and launch: VALU 2 cycles per wave64, transcendental 4, fp64 FMA/MUL/
     ADD 4) / the live HIP-event kernel time; peak = 1024 SIMDs x 2.4 GHz.
     frac_at_held_clock uses the clock the profiled run held instead.  Beside
-    it: the measured HBM traffic (PMC) as GB/s and SURVEY §8(d)'s algorithmic
-    12 B/bin figure, which a fused kernel does not move."""
+    it: the measured HBM traffic (PMC) as GB/s, and SURVEY §8(d)'s nominal
+    12 B/bin (read P, read N, write G) as a byte count only: the fused kernel
+    never writes G and reads the shared rows once per 16-cell workgroup, so
+    those bytes are not moved and are not a bandwidth (as a rate they would
+    exceed the HBM peak); `pmc_traffic_over_nominal` says how much of them
+    the launch really moves."""
     bytes_per_unit = 12 * (n_fft // 2 + 1)
     ks = kern_ms / 1e3
-    alg = units * bytes_per_unit / ks
+    nominal = units * bytes_per_unit
     roof = {"bound": "valu", "achieved": None, "peak": SIMDS * CLOCK / 1e9,
             "unit": "G SIMD issue-cycles/s (1024 SIMDs)", "frac": None, "traffic": None,
             "kernel": f"cse::enhance_kernel<{n_fft}>", "kernel_ms": kern_ms,
             "units_per_launch": units,
-            "hbm_algorithmic_GBps": alg / 1e9, "hbm_algorithmic_frac": alg / HBM_PEAK,
-            "bytes_per_unit_algorithmic": bytes_per_unit,
+            "nominal_unfused_bytes_per_unit": bytes_per_unit,
+            "nominal_unfused_bytes_per_launch": nominal,
+            "nominal_unfused_note": ("SURVEY 8(d)'s 12 B/bin (P, N read, G written, f32) for an "
+                                     "unfused gain kernel; the fused kernel does not move these "
+                                     "bytes, so no bandwidth is derived from them"),
+            "pmc_traffic_over_nominal": None,
             "hbm_measured_GBps": None, "hbm_measured_frac": None,
             "kernel_src_sha": kernel_src_sha()}
     pmc = load_pmc(units, n_fft)
@@ -608,6 +679,7 @@ def roofline_block(n_fft, units, kern_ms):
         roof["traffic"] = tb
         roof["hbm_measured_GBps"] = tb / ks / 1e9
         roof["hbm_measured_frac"] = tb / ks / HBM_PEAK
+        roof["pmc_traffic_over_nominal"] = tb / nominal
     need = pmc.get("valu_issue_cycles")
     if need:
         roof["achieved"] = need / ks / 1e9
@@ -688,18 +760,38 @@ def sweep_block(args, world, total_pairs, weak):
     return out
 
 
-def parity_block(eng, noisy, clean, clean_pow, n_fft, snr_local, cpu_snr, cpu_y, weak):
-    """Device vs oracle on pair 0 (the CPU baseline's pair): the timed step's
-    SNR of every cell the oracle computed, and the waveforms of the stratified
-    cells (recomputed through the same kernel, one launch)."""
+def rank_pair_cells(local_specs, n_fft):
+    """(slot, {grid index: local cell index}) for the pair this rank holds most
+    cells of; grid indices into grid_specs(1, n_fft)."""
+    index = {(alg, tuple(p.items())): g for g, (_, alg, p) in enumerate(grid_specs(1, n_fft))}
+    by_slot = {}
+    for j, (s, alg, p) in enumerate(local_specs):
+        by_slot.setdefault(s, {})[index[(alg, tuple(p.items()))]] = j
+    slot = max(sorted(by_slot), key=lambda s: len(by_slot[s]))
+    return slot, by_slot[slot]
+
+
+def pick_parity_cells(seconds, n_fft, held):
+    """The stratified parity cells this rank holds; when it holds few of them
+    (a partial pair at a shard end), 64 of its held cells at random instead."""
+    cells = [g for g in parity_cells(seconds, n_fft) if g in held]
+    if len(cells) < 16:
+        rng = np.random.default_rng(7)
+        hs = sorted(held)
+        cells = sorted(rng.choice(hs, min(64, len(hs)), replace=False).tolist())
+    return cells
+
+
+def parity_block(eng, noisy1, clean1, clean_pow1, n_fft, dev_snr, cpu_snr, cpu_y):
+    """Device vs oracle on one pair: the timed step's SNR of every cell the
+    oracle computed (dev_snr: grid index -> device SNR), and the waveforms of
+    the stratified cells (recomputed through the same kernel, one launch)."""
     from classical_speech_enhancement_amd.engine import snr_db
     specs0 = grid_specs(1, n_fft)
-    # the plan's first len(specs0) cells are pair 0's grid in grid order (both modes at N=1)
-    d_snr = snr_local[:len(specs0)]
-    ids = sorted(cpu_snr)
-    snr_err = max(abs(d_snr[i] - cpu_snr[i]) for i in ids) if ids else None
+    ids = sorted(i for i in cpu_snr if i in dev_snr)
+    snr_err = max(abs(dev_snr[i] - cpu_snr[i]) for i in ids) if ids else None
     y_ids = sorted(cpu_y)
-    res = eng.run(noisy[:1], [(0, specs0[i][1], specs0[i][2]) for i in y_ids], clean=clean[:1],
+    res = eng.run(noisy1, [(0, specs0[i][1], specs0[i][2]) for i in y_ids], clean=clean1,
                   want_waveforms=True)
     yd = res["y"].double().cpu().numpy()
     e2 = em = 0.0
@@ -708,15 +800,44 @@ def parity_block(eng, noisy, clean, clean_pow, n_fft, snr_local, cpu_snr, cpu_y,
         e2 = max(e2, float(np.linalg.norm(yd[j] - ref) / np.linalg.norm(ref)))
         em = max(em, float(np.max(np.abs(yd[j] - ref)) / np.max(np.abs(ref))))
     # the re-run cells give the timed step's SNR exactly (no cell depends on its batch)
-    rerun_same = bool(np.array_equal(snr_db(res["sse"], clean_pow[0]),
-                                      d_snr[y_ids])) if y_ids else None
+    rerun_same = bool(np.array_equal(snr_db(res["sse"], clean_pow1),
+                                      np.array([dev_snr[i] for i in y_ids]))) if y_ids else None
     ok = (e2 <= TOL and em <= TOL and (snr_err is None or snr_err <= SNR_TOL_DB)
           and rerun_same is not False)
     return {"cells_snr": len(ids), "max_snr_abs_db": snr_err, "snr_tol_db": SNR_TOL_DB,
             "cells_waveform": len(y_ids), "max_rel_l2": e2, "max_rel_max": em, "tol": TOL,
             "waveform_cells_from_timed_launch_snr_identical": rerun_same,
-            "strata": "4 cells per (algorithm, hop, noise method) of pair 0's n_fft grid",
+            "strata": ("4 cells per (algorithm, hop, noise method) of the n_fft grid of the pair "
+                       "the rank holds most cells of"),
             "pass": bool(ok)}
+
+
+PARITY_FIELDS = ("pass", "pair", "cells_snr", "cells_waveform", "max_rel_l2", "max_rel_max",
+                 "max_snr_abs_db")
+
+
+def gather_parity(par, dist_ctx):
+    """Every rank's parity summary on every rank (one all_gather): the line is
+    self-verifying at N > 1 too; "pass" holds only if every rank passed."""
+    import torch
+    dist, coll_dev, world = dist_ctx
+    nan = float("nan")
+    v = torch.tensor([nan if par is None or par.get(k) is None else float(par[k])
+                      for k in PARITY_FIELDS], dtype=torch.float64)
+    if dist is not None:
+        out = torch.empty(world * len(PARITY_FIELDS), dtype=torch.float64, device=coll_dev)
+        dist.all_gather_into_tensor(out, v.to(coll_dev))
+        v = out.cpu()
+    rows = v.numpy().reshape(-1, len(PARITY_FIELDS))
+    per = []
+    for r in rows:
+        d = {k: (None if np.isnan(x) else x) for k, x in zip(PARITY_FIELDS, r.tolist())}
+        d["pass"] = d["pass"] == 1.0
+        for k in ("pair", "cells_snr", "cells_waveform"):
+            d[k] = None if d[k] is None else int(d[k])
+        per.append(d)
+    return {"per_rank": per, "pass": all(d["pass"] for d in per),
+            "ranks_checked": sum(1 for d in per if d["cells_waveform"])}
 
 
 if __name__ == "__main__":

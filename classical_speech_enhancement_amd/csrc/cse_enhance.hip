@@ -97,8 +97,8 @@ __device__ __forceinline__ float mmse_bracket(float v, float sqrtv) {
 // workgroup shares: the row stager computes it once per bin and frame
 // (P * inv with inv = 1/max(N, eps) from cse_noise_invert), and the cells read
 // it from LDS.  The decision-directed recursion only ever uses
-// prev_gain**2 * prev_gamma (wiener_filter.py:133, mmse.py:82,
-// advanced_mmse.py:215): the carried state is rr = (G*G)*gamma.
+// prev_gain**2 * prev_gamma (wiener_filter.py:69, mmse.py:82,
+// advanced_mmse.py:95): the carried state is rr = (G*G)*gamma.
 // ---------------------------------------------------------------------------
 // d = max(gamma - 1, 0) (the ML estimate of the DD rule) is per bin too: the
 // n_fft = 512 stager stores the row (gamma, d) (cells compute d themselves at
@@ -497,7 +497,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     constexpr int F = 2 * HOP / SP;     // samples a lane retires per frame
     constexpr int PEND = 32 - F;        // overlap-add sums carried to the next frame
     static_assert(F >= 2 && F <= 32 && (F % 2) == 0, "hop/n_fft combination");
-    // gamma floor of each algorithm (wiener_filter.py:122, mmse.py:71, advanced_mmse.py:207)
+    // gamma floor of each algorithm (wiener_filter.py:61, mmse.py:74, advanced_mmse.py:90)
     constexpr float EPS = (ALGO == CSE_ALGO_MMSE) ? 1e-12f : 1e-10f;
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
@@ -967,9 +967,10 @@ __device__ __forceinline__ void dispatch_algo(const Args& a, const cse_cell_t* w
 // OUT: the g_out (gain matrix) variant for parity tests; waveform output
 // (y_out, any out_len) is available in both variants at run time.
 template <int NFFT, bool OUT>
-// launch bounds: workgroups per CU such that the register budget allows
-// CSE_WAVES_PER_SIMD waves per SIMD (4 SIMDs per CU)
-__global__ void __launch_bounds__(WG<NFFT>::THREADS, 4 * CSE_WAVES_PER_SIMD / WG<NFFT>::WAVES)
+// launch bounds: HIP's second argument is the minimum number of waves per SIMD
+// (amdgpu_waves_per_eu), whatever the workgroup size: the register budget is
+// 512 / CSE_WAVES_PER_SIMD VGPRs per lane
+__global__ void __launch_bounds__(WG<NFFT>::THREADS, CSE_WAVES_PER_SIMD)
     enhance_kernel(Args a) {
     using W = WG<NFFT>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

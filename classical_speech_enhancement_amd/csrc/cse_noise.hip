@@ -203,7 +203,13 @@ __device__ __forceinline__ double wave_at(const double (&v)[E], int lane, int id
 
 // bin_stats_kernel's median / percentile modes for n2 = 64 E <= 2048 sort
 // slots: one wavefront per (bin, signal), 4 bins per block, the same order
-// statistics and the same arithmetic as the LDS path (bit-identical results)
+// statistics and the same arithmetic as the LDS path: bit-identical results
+// for finite P.  A NaN in P is not propagated the way numpy's median /
+// percentile would (fmin / fmax drop it, so the statistic of the remaining
+// values comes out, and which path runs depends on T <= 2048); such a P
+// comes only from a non-finite noisy signal, whose cells are non-finite in
+// the reference and here alike (the finite[] output), so the estimate's value
+// does not reach any score.
 template <int E>
 __global__ void __launch_bounds__(256) bin_stats_wave_kernel(
     const double* __restrict__ P, int T, int B, int mode, const int* __restrict__ sel, int k,

@@ -77,10 +77,12 @@ static_assert(SSTR >= 8 * SROW && SSTR % 64 == GRP, "staging slot stride");
 // (m < 3, r < 5) = sum over k' < 139 of e[8(q0 + 3a) - 58 + k'] c_r[k' - 8m]:
 // A[row][k'] = the slot's staged sample 24a + k', B[k'][5m + r] = c_r[k' - 8m].
 // The clipped sample is fixed point E = rint(e 2^38) in 5 balanced base-256
-// digits (planes of int8), the coefficient C = rint(c 2^47) in 6; digit pairs
-// i + j <= 5 accumulate exactly in int32 per s = i + j (6 x 139 x 128^2 < 2^31)
-// and out = 2^-53 sum_s acc_s 256^(5 - s) (pairs with i + j >= 6 weigh below
-// 2^-41).  v_mfma_i32_16x16x64_i8: K in 3 chunks of 64 (139 used), 16
+// digits (planes of int8), the coefficient C = rint(c 2^47) in 6; the digit
+// pairs i + j <= MF_S (CSE_STOI_MF_S, default 4) accumulate exactly in int32
+// per s = i + j (6 x 139 x 128^2 < 2^31) and out = 2^-53 sum_s acc_s
+// 256^(5 - s).  The dropped pairs i + j > MF_S weigh below 2^(-33 - 8 (MF_S - 4))
+// of full scale (MF_S = 4: 2^-33; measured 7.4e-11 in STOI against the fp64
+// FIR over 4,096 10-s cells).  v_mfma_i32_16x16x64_i8: K in 3 chunks of 64 (139 used), 16
 // columns (15 used); lane l holds k = 16 (l >> 4) + b of its row / column l & 15
 // (any k map shared by A and B is exact: tools/micro/mfma_i8_layout.hip).
 constexpr int MF_ED = 5, MF_CD = 6, MF_KC = 3;
@@ -88,6 +90,9 @@ constexpr int MF_ED = 5, MF_CD = 6, MF_KC = 3;
 #define CSE_STOI_MF_S 4  // digit pairs kept: i + j <= CSE_STOI_MF_S (4: 7e-11 of the fp64 FIR)
 #endif
 constexpr int MF_S = CSE_STOI_MF_S;
+// Bf[j] indexes the MF_CD coefficient digit planes (j <= MF_S) and the scale
+// 256^(5 - MF_S) must be a non-negative shift
+static_assert(MF_S >= 0 && MF_S <= MF_CD - 1, "CSE_STOI_MF_S must lie in [0, 5]");
 constexpr int MF_PL = 384;                  // bytes per digit plane and slot (>= 24 * 8 + 192)
 constexpr int MF_SL = MF_ED * MF_PL;        // bytes per slot
 constexpr int MF_SLOTS = 7;                 // slots per chunk: 63 rows = 4 tiles, one per wave

@@ -18,12 +18,15 @@
 // packing.
 //
 // Exactness: the fp32 FFT value of every lag is within a small multiple of
-// 1e-6 ||r0|| ||s0|| of the exact one, so every lag within
-// delta = 2e-5 ||r0|| ||s0|| of the fp32 maximum is re-evaluated by a direct
+// 1e-6 ||r0|| ||e|| of the exact one (e the raw head, mean included: the FFT
+// sees it before the mean correction), so every lag within
+// delta = 2e-5 ||r0|| ||e|| of the fp32 maximum is re-evaluated by a direct
 // fp64 sum and the lag is chosen among those (ties -> smallest lag, like
 // np.argmax).  The candidates are marked in an LDS bitmap over the lags and
-// re-evaluated in ascending lag order, however many there are; more than
-// XCAND of them (a flat correlation) only sets status CSE_XCORR_FLAT.
+// re-evaluated in ascending lag order, however many there are: up to XCAND
+// one block sum each, more (a flat correlation, status CSE_XCORR_FLAT) XG
+// lags per pass over the head.  An all-zero head is lag -max_lag directly
+// (every correlation value is 0: np.argmax's first index).
 #include "cse_common.hpp"
 
 #include <type_traits>
@@ -415,7 +418,17 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
         return;
     }
     const double mu = s1 / n;
-    const double snorm = fmax(s2 - n * mu * mu, 0.0);
+    if (s2 == 0.0) {
+        // an all-zero head: sig0 = 0 exactly (its mean is 0), so scipy's
+        // correlation is 0 at every lag and np.argmax takes the first kept
+        // one, lag = -max_lag (no candidate re-evaluation: all 2 L + 1 tie)
+        if (tid == 0) {
+            a.lag[cell] = -L;
+            a.zero_energy[cell] = a.Z[(int64_t)sig * (2 * L + 1)];
+            a.status[cell] = CSE_XCORR_FLAT;
+        }
+        return;
+    }
     // inverse real transform: Zi(f) = (C_f + conj C_{XH-f}) + i e^{+2πi f/XN} (C_f - conj C_{XH-f})
 #pragma unroll
     for (int r = 0; r < 16; ++r) buf[pt + 272 * r] = C[r];
@@ -469,7 +482,11 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     }
     const float cmax = rv[0];
     const int kmax = ri[0];
-    const float delta = (float)(2e-5 * sqrt(a.rnorm[sig] * snorm)) + 1e-30f;
+    // the fp32 FFT works on the raw head (mean included: c = c_raw - mu W), so
+    // its error scales with ||r0|| ||e||, not ||r0|| ||e - mu||: a head with a
+    // large DC and little variance (a DC head: every true c(l) is 0) needs the
+    // raw energy s2 here, or fp32 noise picks the lag
+    const float delta = (float)(2e-5 * sqrt(a.rnorm[sig] * s2)) + 1e-30f;
     if (tid == 0) ncand = 0;
     for (int w = tid; w < XWORDS; w += XT) cbits[w] = 0u;
     __syncthreads();
@@ -485,7 +502,59 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     const int nc = ncand;
     int kbest = kmax;
     const int status = nc > XCAND ? CSE_XCORR_FLAT : CSE_XCORR_OK;
-    if (nc > 1) {
+    if (nc > XCAND) {
+        // a flat correlation (up to 2 L + 1 candidates): XG lags per pass over
+        // the head, each thread's samples m = tid + XT i read once for all of
+        // them, the XG sums reduced together through the idle FFT buffer
+        // (one pass per XG candidates instead of one pass and a block sum
+        // each: r03's uncapped form took ~50 ms for 3,201 candidates)
+        constexpr int XG = 8;
+        const double* r0 = a.r0buf + (int64_t)sig * n;
+        double* rd = (double*)buf;  // [XG][XT]
+        double bestd = -INFINITY;
+        kbest = 0x7fffffff;
+        const int nw = (2 * L + 1 + 31) >> 5;
+        int w = 0;
+        unsigned bits = cbits[0];
+        for (;;) {
+            int ks[XG], ng = 0;
+            while (ng < XG) {  // the next XG candidates in ascending lag order (uniform)
+                while (!bits && ++w < nw) bits = cbits[w];
+                if (!bits) break;
+                ks[ng++] = 32 * w + __builtin_ctz(bits);
+                bits &= bits - 1u;
+            }
+            if (ng == 0) break;
+            double acc[XG];
+#pragma unroll
+            for (int g = 0; g < XG; ++g) acc[g] = 0.0;
+            for (int m = tid; m < n; m += XT) {
+                const double ev = (double)e[m] - mu;
+#pragma unroll
+                for (int g = 0; g < XG; ++g) {
+                    const int q = m + (g < ng ? ks[g] : L) - L;  // r0[m + l] inside [0, n)
+                    if (g < ng && q >= 0 && q < n) acc[g] += r0[q] * ev;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int g = 0; g < XG; ++g) rd[g * XT + tid] = acc[g];
+            __syncthreads();
+            for (int s = XT / 2; s > 0; s >>= 1) {
+                if (tid < s)
+#pragma unroll
+                    for (int g = 0; g < XG; ++g) rd[g * XT + tid] += rd[g * XT + tid + s];
+                __syncthreads();
+            }
+            for (int g = 0; g < ng; ++g) {
+                const double v = rd[g * XT];
+                if (v > bestd) {  // ascending lags: the first maximum is kept
+                    bestd = v;
+                    kbest = ks[g];
+                }
+            }
+        }
+    } else if (nc > 1) {
         // exact fp64 re-evaluation of every candidate, in ascending lag order
         // (the bitmap words are read by every thread alike: uniform control
         // flow around block_sum's barriers):

@@ -78,7 +78,7 @@ def noise_key(alg, params, T):
       - mmse/omlsa smooth any time-varying estimate except true_noise
         (mmse.py:48-54, advanced_mmse.py:60-66); mu=None means no smoothing;
       - inverse: Wiener/MMSE/OMLSA read 1/max(N, eps) (their in-loop floor,
-        wiener_filter.py:122, mmse.py:71, advanced_mmse.py:207), SS reads N.
+        wiener_filter.py:58, mmse.py:71, advanced_mmse.py:87), SS reads N.
     A key is static (one [B] row for all frames) iff expand is False and the
     method is percentile/simple.
     """

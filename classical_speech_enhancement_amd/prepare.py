@@ -60,6 +60,13 @@ def shift_by_lag(sig, lag):
 def alignment_lag(ref, sig, sr=16000, engine=None):
     """The align_to_reference lag of ``sig`` against ``ref`` computed on the
     device (None when the reference skips alignment: fewer than 256 samples)."""
+    return alignment_lag_status(ref, sig, sr, engine)[0]
+
+
+def alignment_lag_status(ref, sig, sr=16000, engine=None):
+    """(lag, cse_xcorr_lag status) — alignment_lag plus the status word
+    (_lib.XCORR_OK, XCORR_FLAT: more than 64 near-maximal lags were
+    re-evaluated in fp64); (None, None) below 256 samples."""
     import torch
     from .engine import Engine
     eng = engine or Engine()
@@ -67,7 +74,7 @@ def alignment_lag(ref, sig, sr=16000, engine=None):
     sig = np.asarray(sig, dtype=np.float64)
     n = int(min(len(ref), len(sig), ALIGN_CORR_SAMPLES * sr // 16000))
     if n < ALIGN_MIN_SAMPLES:
-        return None
+        return None, None
     max_lag = min(int(0.10 * sr), n - 1, ALIGN_MAX_LAG)
     lib, dev = eng.lib, eng.device
     c = torch.as_tensor(ref[:n]).to(dev).view(1, -1)
@@ -86,7 +93,7 @@ def alignment_lag(ref, sig, sr=16000, engine=None):
                                  _ptr(lag), _ptr(zero), _ptr(status), None, st), "cse_xcorr_lag")
     if int(status.item()) == _lib.XCORR_NONFINITE:
         raise ValueError("alignment: non-finite samples in the signal")
-    return int(lag.item())
+    return int(lag.item()), int(status.item())
 
 
 def prepare_pair(clean, sr_c, noisy, sr_n, target_sr=16000, do_align=True, engine=None):

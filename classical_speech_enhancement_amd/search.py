@@ -14,7 +14,8 @@ Here the whole (pair x algorithm x grid cell) set is one job:
                  (SURVEY §8(e)'s cost model): whole pairs per rank, so each
                  pair's STFT and noise PSDs run on one rank (two at a cut)
   run_grid       each rank computes its cells (Engine on its GPU), then ONE
-                 all_gather of fixed-size records {cell_id, sse, snr, finite, stoi}
+                 all_gather of fixed-size 56-B records (RECORD_FIELDS: cell_id,
+                 sse, snr, finite, stoi, lag, xstatus; a 6-column table)
                  (RCCL over xGMI for backend "nccl", gloo in CPU tests)
   select_best    rank 0's sequential best-so-far scan in grid order
                  (speech_enhancement_comparison.py:183-216) — NOT an argmax:
@@ -484,7 +485,7 @@ def _opt(v):
 def optimize_parameters(clean_reference, noisy_audio, sr, algorithm, param_ranges=None,
                         compute=None, stoi_fn=None):
     """Single-pair, single-algorithm mirror of the reference's
-    optimize_parameters (speech_enhancement_comparison.py:108-263), scored by
+    optimize_parameters (speech_enhancement_comparison.py:109-252), scored by
     STOI and SNR: returns {'stoi': {'score', 'params', 'cell', 'snr'},
     'snr': {'score', 'params', 'cell', 'stoi'}, 'baseline': {'stoi', 'snr'},
     'improvements': {'stoi', 'snr'}, 'table'}; raises ValueError like :251-253

@@ -222,7 +222,7 @@ int cse_noise_finish(const cse_noise_job_t* jobs, int n_jobs, int64_t n_sig, int
 /*
  * out = 1 / max(N, eps) (fp64 math, f32 out), n elements: the noise row the
  * Wiener/MMSE/OMLSA cells of cse_enhance_cells read (their in-loop floors,
- * wiener_filter.py:122, mmse.py:71, advanced_mmse.py:207, folded in).
+ * wiener_filter.py:58, mmse.py:71, advanced_mmse.py:87, folded in).
  */
 int cse_noise_invert(const float* N, int64_t n, double eps, float* out, cse_stream_t stream);
 

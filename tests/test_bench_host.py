@@ -1,0 +1,115 @@
+"""bench.py's host-side multi-rank instrumentation on CPU: which pair a rank
+checks and which of its cells, and the per-rank stats / parity gathers over
+world_size 2 (gloo), the way the 8-GPU node runs them over RCCL."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import bench
+from classical_speech_enhancement_amd import search
+from classical_speech_enhancement_amd.parameter_ranges import grid_specs
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+class _Args:
+    seconds = 10.0
+    pairs = None
+    pairs_total = 100
+
+
+@pytest.mark.parametrize("world", [1, 8])
+def test_rank_pair_cells_cover_the_rank_s_most_held_pair(world):
+    """rank_job's local specs -> the pair slot a rank checks and the grid index
+    of each held cell (grid_specs(1, 512) order, the oracle's cell order)."""
+    g512 = grid_specs(1, 512)
+    for rank in range(world):
+        pair_ids, local, gids, _, _ = bench.rank_job(_Args, world, rank, 512)
+        slot, held = bench.rank_pair_cells(local, 512)
+        counts = {}
+        for s, _, _ in local:
+            counts[s] = counts.get(s, 0) + 1
+        assert len(held) == max(counts.values())
+        for g, j in held.items():
+            s, alg, p = local[j]
+            assert s == slot and (alg, p) == (g512[g][1], g512[g][2])
+            # the global cell id is pair-major grid order
+            assert gids[j] == pair_ids[slot] * len(g512) + g
+        cells = bench.pick_parity_cells(10.0, 512, held)
+        assert 16 <= len(cells) <= 64 and all(c in held for c in cells)
+        if world == 1:
+            assert slot == 0 and pair_ids[slot] == 0 and len(cells) == 64
+
+
+def _rank(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+        ctx = (dist, torch.device("cpu"), world)
+        st = {"wall_s": 1.0 + rank, "kernel_ms": 10.0 * (rank + 1), "analysis_ms": 2.0,
+              "units": 100 + rank, "cells": 7, "pairs": 3}
+        r = bench.gather_rank_stats(st, ctx)
+        par = {"pass": rank == 0, "pair": 5 + rank, "cells_snr": 64, "cells_waveform": 64,
+               "max_rel_l2": 1e-7 * (rank + 1), "max_rel_max": 2e-7, "max_snr_abs_db": None}
+        p = bench.gather_parity(par, ctx)
+        np.save(os.path.join(out, f"r{rank}.npy"),
+                np.array([r["imbalance_max_over_mean"]["kernel_ms"],
+                          r["imbalance_max_over_mean"]["wall_s"],
+                          sum(x["units"] for x in r["per_rank"]),
+                          float(p["pass"]), p["per_rank"][1]["pair"],
+                          p["per_rank"][1]["max_rel_l2"], p["ranks_checked"],
+                          float(p["per_rank"][0]["max_snr_abs_db"] is None)]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rank_stats_and_parity_gather_world2(tmp_path):
+    import torch.multiprocessing as tmp
+    tmp.spawn(_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    a, b = np.load(tmp_path / "r0.npy"), np.load(tmp_path / "r1.npy")
+    assert np.array_equal(a, b)  # every rank sees the same gathered figures
+    assert a[0] == pytest.approx(20.0 / 15.0) and a[1] == pytest.approx(2.0 / 1.5)
+    assert a[2] == 201
+    assert a[3] == 0.0  # rank 1 failed: the line fails
+    assert a[4] == 6 and a[5] == pytest.approx(2e-7) and a[6] == 2 and a[7] == 1.0
+
+
+def test_single_process_gathers_need_no_process_group():
+    import torch
+    ctx = (None, torch.device("cpu"), 1)
+    r = bench.gather_rank_stats({"wall_s": 1.0, "kernel_ms": 3.0, "analysis_ms": 1.0,
+                                 "units": 10, "cells": 2, "pairs": 1}, ctx)
+    assert r["imbalance_max_over_mean"]["kernel_ms"] == 1.0 and r["per_rank"][0]["units"] == 10
+    p = bench.gather_parity(None, ctx)
+    assert not p["pass"] and p["ranks_checked"] == 0
+
+
+def test_roofline_block_prints_no_bandwidth_from_nominal_bytes():
+    roof = bench.roofline_block(512, 457237200, 170.0)
+    assert roof["nominal_unfused_bytes_per_launch"] == 457237200 * 3084
+    assert not any("algorithmic_GBps" in k or "algorithmic_frac" in k for k in roof)
+    for k, v in roof.items():
+        if k.endswith("GBps") and v is not None:
+            assert v < 8000.0, (k, v)
+    if roof.get("traffic"):
+        assert 0 < roof["pmc_traffic_over_nominal"] < 1
+
+
+def test_job_units_match_shards():
+    specs = search.job_specs(100, n_fft=512)
+    total = 0
+    for rank in range(8):
+        _, local, _, units, _ = bench.rank_job(_Args, 8, rank, 512)
+        total += len(local)
+    assert total == len(specs) and units == 100 * 4572372

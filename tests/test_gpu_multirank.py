@@ -50,6 +50,9 @@ def test_bench_two_ranks_weak_scaling(gpu):
     units = d["config"]["units_per_step"]  # both ranks' pairs
     assert units == 2 * d["config"]["units_per_step_rank0"]
     assert d["value"] == pytest.approx(units / (d["ms_per_step"] / 1e3), rel=1e-6)
+    rk = d["ranks"]["per_rank"]
+    assert [r["units"] for r in rk] == [units // 2] * 2 and [r["pairs"] for r in rk] == [1, 1]
+    assert d["parity"]["pass"] and [p["pair"] for p in d["parity"]["per_rank"]] == [0, 1]
 
 
 def _rank(rank, world, port, outdir):
@@ -160,10 +163,14 @@ def test_bench_eight_ranks_strong_scaling_rehearsal(gpu, tmp_path):
     the card: BASELINE config 4's 100-pair job sharded by search.assign_shards.
     The line counts the whole job once, each rank holds at most 14 pairs (whole
     pairs plus a part at each end of its run), and the gathered per-cell
-    records equal a world-1 run's bit for bit."""
+    records equal a world-1 run's bit for bit.  The line is instrumented for the
+    first hardware run: per-rank kernel / analysis / wall time, units, cells
+    and pairs with their max / mean spread, and a parity check on every rank
+    (its most-held pair's stratified cells against the oracle)."""
     common = ["--steps", "1", "--warmup", "1", "--pairs-total", "100", "--full-grid-steps", "0",
-              "--no-sweep", "--no-cpu-baseline", "--no-parity"]
-    env = dict(os.environ, CSE_DIST_BACKEND="gloo")
+              "--no-sweep", "--no-cpu-baseline"]
+    # 8 ranks share this box's CPU share: 2 oracle processes each
+    env = dict(os.environ, CSE_DIST_BACKEND="gloo", CSE_CPU_BASELINE_PROCS="2")
     t8, t1 = tmp_path / "t8.npy", tmp_path / "t1.npy"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
@@ -178,11 +185,25 @@ def test_bench_eight_ranks_strong_scaling_rehearsal(gpu, tmp_path):
     assert abs(d["config"]["units_per_step_rank0"] - 100 * 4572372 / 8) < 0.02 * 100 * 4572372 / 8
     assert d["value"] == pytest.approx(d["config"]["units_per_step"] / (d["ms_per_step"] / 1e3),
                                        rel=1e-6)
-    one = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--dump-table", str(t1)]
-                         + common, cwd=REPO, capture_output=True, text=True, timeout=420)
+    rk = d["ranks"]["per_rank"]
+    assert len(rk) == 8
+    assert sum(r["units"] for r in rk) == d["config"]["units_per_step"]
+    assert sum(r["cells"] for r in rk) == 487200
+    assert all(r["kernel_ms"] > 0 and r["analysis_ms"] > 0 and r["wall_s"] > 0 and
+               1 <= r["pairs"] <= 14 for r in rk)
+    imb = d["ranks"]["imbalance_max_over_mean"]
+    assert 1.0 <= imb["units"] < 1.02 and imb["kernel_ms"] >= 1.0 and imb["wall_s"] >= 1.0
+    par = d["parity"]
+    assert par["pass"] and par["ranks_checked"] == 8 and len(par["per_rank"]) == 8
+    assert len({p["pair"] for p in par["per_rank"]}) == 8  # each rank checks a pair of its own
+    assert all(p["cells_waveform"] >= 16 and p["max_rel_l2"] <= 1e-5 for p in par["per_rank"])
+    one = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--dump-table", str(t1),
+                          "--no-parity"] + common, cwd=REPO, capture_output=True, text=True,
+                         timeout=420)
     assert one.returncode == 0, one.stderr[-3000:]
     a, b = np.load(t8), np.load(t1)
     assert a.shape == b.shape == (487200, 2)
     assert np.array_equal(a, b)
     print("8-rank rehearsal:", d["config"]["parallelism"], "pairs on rank 0:",
-          d["config"]["pairs_rank0"], "ms/step", d["ms_per_step"])
+          d["config"]["pairs_rank0"], "ms/step", d["ms_per_step"], "spread", imb,
+          "parity", [(p["pair"], p["max_rel_l2"]) for p in par["per_rank"]])

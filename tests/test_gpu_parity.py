@@ -256,6 +256,54 @@ def test_alignment_lags_10s_vs_oracle(P):
         assert abs(snr_db(res["sse"][j:j + 1], ps)[0] - ref) < 2e-4, (name, p)
 
 
+@pytest.mark.parametrize("case", ["zero", "dc", "dc_noise", "tone", "shift40"])
+def test_alignment_flat_and_periodic_heads(P, case):
+    """Heads whose correlation with the clean head is flat (more than 64 lags
+    within the fp32 margin of the maximum: every one re-evaluated in fp64, XG
+    lags per pass) or periodic, against the oracle's align_lag
+    (speech_enhancement_comparison.py:38-69; np.argmax takes the first of
+    equal values):
+      zero      all-zero head: every c(l) is 0 -> lag -max_lag (early out);
+      dc        a constant head: sig0 = 0 exactly, c(l) = 0 -> lag -max_lag,
+                though the fp32 FFT sees the raw 0.25 (its error scales with
+                the raw energy, which the candidate margin must use);
+      dc_noise  0.5 + 1e-4 noise: all 3,201 lags within the margin, the
+                fp64 re-evaluation picks the true maximum;
+      tone      a 37-sample-period sinusoid: periodic peaks;
+      shift40   the clean signal delayed by 40 samples (f32): lag -40.
+    The worst-case time per cell (3,201 candidates) is printed."""
+    import time
+    import torch
+    from classical_speech_enhancement_amd import _lib
+    from classical_speech_enhancement_amd.engine import Engine
+    from classical_speech_enhancement_amd.prepare import alignment_lag_status
+    clean, _ = make_pair(3, 3.0)
+    n = len(clean)
+    rng = np.random.default_rng(5)
+    head = {
+        "zero": np.zeros(n),
+        "dc": np.full(n, 0.25),
+        "dc_noise": 0.5 + 1e-4 * rng.standard_normal(n),
+        "tone": 0.3 * np.sin(2 * np.pi * np.arange(n) / 37.0),
+        "shift40": np.roll(clean, 40),
+    }[case].astype(np.float32).astype(np.float64)
+    eng = Engine()
+    ref = oracle.align_lag(clean, head, 16000)
+    alignment_lag_status(clean, head, 16000, eng)  # warm (workspace, first launch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lag, status = alignment_lag_status(clean, head, 16000, eng)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(f"{case}: lag {lag} (oracle {ref}), status {status}, {dt * 1e3:.2f} ms per call")
+    assert lag == ref, (case, lag, ref)
+    if case in ("zero", "dc", "dc_noise"):
+        assert status == _lib.XCORR_FLAT and lag == (-1600 if case != "dc_noise" else lag)
+    if case == "shift40":
+        assert lag == -40 and status == _lib.XCORR_OK
+    assert dt < 0.25  # one cell, prepare included; r03's uncapped loop took ~50 ms alone
+
+
 @pytest.mark.parametrize("length", [4993, 7999, 9985])
 def test_alignment_odd_and_block_edge_lengths(P, length):
     """Correlated heads of odd length and of one sample past a 4992-sample
@@ -424,3 +472,47 @@ def test_noise_params_and_short_clean_match_reference_golden(P):
             assert rel_l2(y, g[key]) <= TOL and rel_max(y, g[key]) <= TOL, key
             n += 1
     assert n == 24
+
+
+@pytest.mark.parametrize("T_sec", [1.0, 20.0])
+def test_percentile_pairs_equal_single_estimates(P, T_sec):
+    """cse_noise_percentile_med2 (two percentiles sharing one eps: the frame
+    energies once, then each percentile's selection and statistic) against
+    cse_noise_percentile_med at the same eps, bit for bit: both outputs of a
+    pair, and the odd estimate of a group (N_b = NULL), at T = 126 and 2,501
+    (the wave-sort and LDS-sort statistic paths: T <= 2048 and above), plus the oracle's
+    PercentileNoiseEstimator (noise_estimation.py:20-56) to 1e-6."""
+    import torch
+    from classical_speech_enhancement_amd import _lib
+    from classical_speech_enhancement_amd.engine import Engine, _ptr, _stream
+    eng = Engine()
+    lib = eng.lib
+    clean, noisy = make_pair(2, T_sec)
+    x = torch.as_tensor(np.stack([noisy, clean])).cuda()
+    _, Pw = eng.stft(x, 512, 128, want_y=False)
+    S, T, B = Pw.shape
+    med = torch.empty((S, B), dtype=torch.float64, device="cuda")
+    ws = torch.empty(int(lib.cse_noise_workspace_bytes(S, T, B)), dtype=torch.uint8, device="cuda")
+    st = _stream()
+    _lib.check(lib.cse_noise_median(_ptr(Pw), S, T, B, _ptr(med), st), "median")
+    for eps in (1e-10, 1e-12):
+        one = {}
+        for pct in (10.0, 20.0):
+            o = torch.empty((S, B), dtype=torch.float32, device="cuda")
+            _lib.check(lib.cse_noise_percentile_med(_ptr(Pw), _ptr(med), S, T, B, pct, eps, _ptr(o),
+                                                    _ptr(ws), st), "med")
+            one[pct] = o.cpu().numpy()
+        a = torch.empty((S, B), dtype=torch.float32, device="cuda")
+        b = torch.empty((S, B), dtype=torch.float32, device="cuda")
+        _lib.check(lib.cse_noise_percentile_med2(_ptr(Pw), _ptr(med), S, T, B, 10.0, 20.0, eps,
+                                                 _ptr(a), _ptr(b), _ptr(ws), st), "med2")
+        assert np.array_equal(a.cpu().numpy(), one[10.0]) and np.array_equal(b.cpu().numpy(), one[20.0])
+        c = torch.full((S, B), -1.0, dtype=torch.float32, device="cuda")
+        _lib.check(lib.cse_noise_percentile_med2(_ptr(Pw), _ptr(med), S, T, B, 20.0, 0.0, eps,
+                                                 _ptr(c), None, _ptr(ws), st), "med2 odd")
+        assert np.array_equal(c.cpu().numpy(), one[20.0])
+        for s in range(S):
+            Pc = Pw[s].cpu().numpy().T  # (B, T) as the reference's estimator takes it
+            for pct in (10.0, 20.0):
+                ref = oracle.percentile_noise(Pc, eps=eps, percentile=pct)
+                assert rel_l2(one[pct][s], np.ravel(ref)) < 1e-6, (T_sec, eps, s, pct)
