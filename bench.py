@@ -690,6 +690,8 @@ def roofline_block(n_fft, units, kern_ms):
         if pmc.get("clock_ghz_profiled"):
             roof["clock_ghz_profiled"] = pmc["clock_ghz_profiled"]
             roof["frac_at_held_clock"] = pmc.get("valu_frac")
+        if pmc.get("valu_issue_cycles_source"):
+            roof["issue_cycles_source"] = pmc["valu_issue_cycles_source"]
         for k in ("share_wait_inst_any", "lds_conflict_cycles_per_lds_inst", "vgprs"):
             if pmc.get(k) is not None:
                 roof[k] = pmc[k]

@@ -166,4 +166,149 @@ __device__ __forceinline__ void idft16(cf (&v)[16]) {
     for (int i = 0; i < 16; ++i) v[i] = t[i];
 }
 
+// ----------------------------------------------------------------------------
+// Packed f32 pairs.  gfx950 executes v_pk_fma/mul/add_f32 (two f32 lanes per
+// instruction) at the SIMD's scalar f32 rate, but a wave issues one VALU
+// instruction per 4 cycles at most: a packed instruction retires two f32
+// operations in that slot, so a kernel whose few resident waves cannot keep
+// the SIMD busy issues half the instructions for its pairable work.  Complex
+// numbers are natural pairs (re, im); the gain kernel also pairs the two
+// mirror bins (k, M - k) a lane owns.  The compiler folds lane swaps and
+// broadcasts (op_sel) and whole-pair negation into the instruction; a
+// negation of one lane it does not fold, so those forms are FMAs against a
+// constant pair (held in SGPRs) or, for a product with a run-time rotor,
+// inline assembly.
+// ----------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 pdup(float s) { return f2{s, s}; }
+
+// Forms with a negation of one lane, written out: the compiler would take a
+// constant pair such as (-1, 1) from two SGPRs for each (and the kernel ran out
+// of SGPRs); VOP3P's op_sel / neg_lo / neg_hi do it in the instruction.
+#define CSE_PK2(name, mods, expr)                                          \
+    __device__ __forceinline__ f2 name(f2 a, f2 b) {                      \
+        f2 r;                                                              \
+        asm("v_pk_add_f32 %0, %1, %2 " mods : "=v"(r) : "v"(a), "v"(b)); \
+        return r;                                                          \
+    }
+// a + i b = (a.x - b.y, a.y + b.x);  a - i b = (a.x + b.y, a.y - b.x)
+CSE_PK2(p_addi, "op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]", )
+CSE_PK2(p_subi, "op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]", )
+// conj(a) + i conj(b) = (a.x + b.y, -a.y + b.x)
+CSE_PK2(p_conj_addi, "op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[1,0]", )
+#undef CSE_PK2
+// (b.x - b.y, b.x + b.y) and (-b.x - b.y, b.x - b.y): r2-scaled rho b of idft4_tw
+__device__ __forceinline__ f2 p_rot1(f2 b) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1] neg_lo:[0,1]" : "=v"(r) : "v"(b));
+    return r;
+}
+__device__ __forceinline__ f2 p_rot3(f2 b) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1] neg_lo:[1,1] neg_hi:[0,1]" : "=v"(r) : "v"(b));
+    return r;
+}
+// c + i k b = (c.x - k b.y, c.y + k b.x) and c - i k b, k a broadcast pair
+__device__ __forceinline__ f2 p_fma_i(f2 b, f2 k, f2 c) {
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[1,0,0]"
+        : "=v"(r) : "v"(b), "s"(k), "v"(c));
+    return r;
+}
+__device__ __forceinline__ f2 p_fma_mi(f2 b, f2 k, f2 c) {
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_hi:[1,0,0]"
+        : "=v"(r) : "v"(b), "s"(k), "v"(c));
+    return r;
+}
+// c + (b.x s, -b.y s) and c + (-b.x s, b.y s), s = the hi lane of g:
+// X_k +/- conj(X_{M-k}) with X_{M-k} = b g.y
+__device__ __forceinline__ f2 p_fma_conj_hi(f2 b, f2 g, f2 c) {
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_hi:[0,1,0]"
+        : "=v"(r) : "v"(b), "v"(g), "v"(c));
+    return r;
+}
+__device__ __forceinline__ f2 p_fms_conj_hi(f2 b, f2 g, f2 c) {
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_lo:[0,1,0]"
+        : "=v"(r) : "v"(b), "v"(g), "v"(c));
+    return r;
+}
+// complex a * w, w known at compile time: (a.x w.x - a.y w.y, a.x w.y + a.y w.x)
+__device__ __forceinline__ f2 p_cmulc(f2 a, float c, float s) {
+    return pfma(a.yy, f2{-s, c}, a.xx * f2{c, s});
+}
+// complex a * w for a run-time w: v_pk_mul_f32 + v_pk_fma_f32 whose lo lane
+// reads -w.y (neg_lo)
+__device__ __forceinline__ f2 p_cmul(f2 a, f2 w) {
+    const f2 t = a.xx * w;  // (a.x w.x, a.x w.y)
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r)
+        : "v"(a), "v"(w), "v"(t));
+    return r;
+}
+
+// idft4 / idft4_tw / idft16 on packed complex values: the same operations
+// as the scalar forms above, one packed instruction per complex addition or
+// per FMA pair (74 instructions per DFT16 instead of 148)
+__device__ __forceinline__ void idft4_pk(f2& a0, f2& a1, f2& a2, f2& a3) {
+    const f2 s02 = a0 + a2, d02 = a0 - a2;
+    const f2 s13 = a1 + a3, e13 = a1 - a3;
+    a0 = s02 + s13;
+    a2 = s02 - s13;
+    a1 = p_addi(d02, e13);
+    a3 = p_subi(d02, e13);
+}
+
+template <int N1>
+__device__ __forceinline__ void idft4_tw_pk(f2& a0, f2& a1, f2& a2, f2& a3) {
+    constexpr float r2 = 0.70710678118654752f;
+    constexpr float c1 = 0.92387953251128674f, s1 = 0.38268343236508978f;
+    constexpr float C = N1 == 1 ? c1 : (N1 == 2 ? r2 : s1);
+    constexpr float TAU = N1 == 1 ? s1 / c1 : (N1 == 2 ? 1.0f : c1 / s1);
+    const f2 b0 = a0, b1 = a1, b2 = a2, b3 = a3;
+    f2 s02, d02, p, m;
+    if (N1 == 2) {  // rho = i
+        s02 = p_addi(b0, b2);
+        d02 = p_subi(b0, b2);
+        p = p_addi(b1, b3);
+        m = p_subi(b1, b3);
+    } else {
+        // q = rho b / r2: (b.x - b.y, b.x + b.y) (N1 = 1), (-b.x - b.y, b.x - b.y) (3)
+        const f2 q2 = N1 == 1 ? p_rot1(b2) : p_rot3(b2);
+        const f2 q3 = N1 == 1 ? p_rot1(b3) : p_rot3(b3);
+        s02 = pfma(pdup(r2), q2, b0);
+        d02 = pfma(-pdup(r2), q2, b0);
+        p = pfma(pdup(r2), q3, b1);
+        m = pfma(-pdup(r2), q3, b1);
+    }
+    // g = p (1 + i TAU), h = m (1 + i TAU)
+    const f2 g = N1 == 2 ? p_addi(p, p) : p_fma_i(p, pdup(TAU), p);
+    const f2 h = N1 == 2 ? p_addi(m, m) : p_fma_i(m, pdup(TAU), m);
+    a0 = pfma(pdup(C), g, s02);
+    a2 = pfma(-pdup(C), g, s02);
+    a1 = p_fma_i(h, pdup(C), d02);   // d02 + i C h
+    a3 = p_fma_mi(h, pdup(C), d02);  // d02 - i C h
+}
+
+__device__ __forceinline__ void idft16_pk(f2 (&v)[16]) {
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) idft4_pk(v[k2], v[4 + k2], v[8 + k2], v[12 + k2]);
+    idft4_pk(v[0], v[1], v[2], v[3]);
+    idft4_tw_pk<1>(v[4], v[5], v[6], v[7]);
+    idft4_tw_pk<2>(v[8], v[9], v[10], v[11]);
+    idft4_tw_pk<3>(v[12], v[13], v[14], v[15]);
+    f2 t[16];
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1)
+#pragma unroll
+        for (int n2 = 0; n2 < 4; ++n2) t[n1 + 4 * n2] = v[4 * n1 + n2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = t[i];
+}
+
 }  // namespace cse

@@ -28,6 +28,12 @@
 #ifndef CSE_JIT_TABLES
 #define CSE_JIT_TABLES 0  // experiment: table reads just before use (register pressure)
 #endif
+#ifndef CSE_PK
+#define CSE_PK 1  // n_fft 512: packed f32 (v_pk_*) gain pairs, packing and DFTs
+#endif
+#ifndef CSE_PK_1024
+#define CSE_PK_1024 0  // the same at n_fft 1024 (r04: 53.3 against 52.8 ms at 13 pairs, so off)
+#endif
 #ifndef CSE_ROT_TABLE_1024
 #define CSE_ROT_TABLE_1024 0  // 1024: packing rotors as base x W32^j (the table measured slower)
 #endif
@@ -229,6 +235,8 @@ struct WG {
     // (gamma, d) / (N, P) float2 [B] at 512); A (float [B], 512: MMSE's
     // c/(gamma + 1e-12), SS's 1/|Y|); clean (float [HMAX])
     static constexpr bool R2 = (NFFT == 512);
+    // packed pairs (CSE_PK): the rows in mirror-pair order, 16-B records
+    static constexpr bool PK = R2 ? CSE_PK : CSE_PK_1024;
     static constexpr int YROW = ((G::B * 8 + 15) / 16) * 16;      // bytes of one Y row
     static constexpr int GROW = ((G::B * (R2 ? 8 : 4) + 15) / 16) * 16;
     static constexpr int AROW = R2 ? ((G::B * 4 + 15) / 16) * 16 : 0;
@@ -362,6 +370,181 @@ __device__ __forceinline__ float gain_bin(float2& y, RowV rv, float& rr, float a
                        cp.lg2_floor - kLsaC, cp.q_spp, cp.p4 * kLog2e);
     }
     return g;
+}
+
+// ---------------------------------------------------------------------------
+// Packed gain of one mirror pair (bins k, M - k) at n_fft 512 (CSE_PK): the
+// same operations as gain_wiener / gain_mmse / gain_omlsa on the two bins at
+// once, every multiply/add/FMA one v_pk_* instruction; max/med3/min and the
+// transcendentals stay per bin (gfx950 has no packed forms of them).  The
+// rows are in pair order (the stager's layout): gam = (gamma_k, gamma_{M-k})
+// (OMLSA: times log2 e), d = (d_k, d_{M-k}), a = MMSE's (c/(gamma + 1e-12))
+// pair.  Returns the pair's gains; rr is the pair's decision-directed state.
+// ---------------------------------------------------------------------------
+#ifndef CSE_PK_HORNER
+#define CSE_PK_HORNER 1  // r04: scalar chains 24.1 against 23.1 ms at 13 pairs (512)
+#endif
+// a polynomial on both lanes: packed (coefficients from SGPR pairs) or as two
+// scalar chains (coefficients as instruction literals, no SGPRs)
+template <int N>
+__device__ __forceinline__ f2 horner2(const float (&c)[N], f2 t) {
+    if (!CSE_PK_HORNER) return f2{horner(c, t.x), horner(c, t.y)};
+    f2 acc = pdup(c[N - 1]);
+#pragma unroll
+    for (int k = N - 2; k >= 0; --k) acc = pfma(acc, t, pdup(c[k]));
+    return acc;
+}
+__device__ __forceinline__ f2 prcp(f2 x) { return f2{fast_rcp(x.x), fast_rcp(x.y)}; }
+__device__ __forceinline__ f2 pmed3(f2 x, float lo, float hi) {
+    return f2{__builtin_amdgcn_fmed3f(x.x, lo, hi), __builtin_amdgcn_fmed3f(x.y, lo, hi)};
+}
+__device__ __forceinline__ f2 pmax(f2 x, float lo) { return f2{fmaxf(x.x, lo), fmaxf(x.y, lo)}; }
+
+template <int NFFT, int ALGO>
+__device__ __forceinline__ f2 gain_pair(f2 gam, f2 d, f2 a, f2& rr, float alpha_t, const CellParam& cp) {
+    constexpr bool R2 = (NFFT == 512);
+    // dd = (1 - alpha_t) max(gamma - 1, 0): the stager's d row at 512; at 1024
+    // max((1 - alpha_t) gamma - (1 - alpha_t), 0) (OMLSA's gamma carries log2 e)
+    const float a_d = 1.0f - alpha_t;
+    f2 dd;
+    if constexpr (R2) {
+        dd = d * pdup(a_d);
+    } else {
+        dd = pmax(pfma(gam, pdup(ALGO == CSE_ALGO_OMLSA ? a_d * kLn2 : a_d), pdup(-a_d)), 0.0f);
+    }
+    if (ALGO == CSE_ALGO_WIENER) {
+        const f2 xi = pmax(pfma(pdup(alpha_t), rr, dd), 1e-10f);
+        const f2 g = pmed3(xi * prcp(xi + 1.0f), cp.p1, 1.0f);
+        rr = (g * g) * gam;
+        return g;
+    } else if (ALGO == CSE_ALGO_MMSE) {
+        const f2 cig = R2 ? a : prcp(gam + 1e-12f) * pdup(0.88622692545275801f);
+        const f2 xi = pmax(pfma(pdup(alpha_t), rr, dd), cp.p1);
+        const f2 v = pmed3((xi * gam) * prcp(xi + 1.0f), 1e-12f, 80.0f);
+        const f2 sv = f2{__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
+        // mmse_bracket on the pair
+        const f2 ta = pfma(v, pdup(0.5f), pdup(-1.0f));  // (v - 2)/2
+        const f2 u = prcp(v);
+        const f2 tb = pfma(u, pdup(2.0f / (CSE_HB_U1 - CSE_HB_U0)),
+                           pdup(-(CSE_HB_U0 + CSE_HB_U1) / (CSE_HB_U1 - CSE_HB_U0)));
+        const f2 pa = horner2(CSE_HA, ta);
+        const f2 pb = sv * horner2(CSE_HB, tb);
+        const f2 h = f2{v.x <= 4.0f ? pa.x : pb.x, v.y <= 4.0f ? pa.y : pb.y};
+        const f2 g = pmed3((sv * cig) * h, cp.p2, cp.p3);
+        rr = (g * g) * gam;
+        return g;
+    } else {  // OMLSA, see gain_omlsa
+        const f2 xi = pmax(pfma(pdup(alpha_t * kLn2), rr, dd), cp.p1);
+        const f2 r = prcp(xi + 1.0f);
+        const f2 xr = xi * r;
+        const float vmax2 = cp.p4 * kLog2e;
+        const f2 v2 = pmed3(xr * gam, 1e-12f * kLog2e, vmax2);
+        const f2 vc2 = f2{fminf(v2.x, CSE_LSA_VMAX2), fminf(v2.y, CSE_LSA_VMAX2)};
+        const f2 pn = horner2(CSE_LSAP, vc2);
+        const f2 dn = horner2(CSE_LSAD, vc2);
+        const f2 xs = xr * f2{__builtin_amdgcn_rsqf(vc2.x), __builtin_amdgcn_rsqf(vc2.y)};
+        const f2 L = f2{fast_log2(xs.x), fast_log2(xs.y)};
+        const f2 ev = f2{fast_exp2(v2.x), fast_exp2(v2.y)};
+        const f2 A = pfma(pdup(cp.q_spp), r * ev, pdup(1e-10f));
+        const f2 num = pfma(L - pdup(cp.lg2_floor - kLsaC), dn, pn);
+        const f2 den = (A + pdup(1.0f - cp.q_spp)) * dn;
+        const f2 e = pfma(A * num, prcp(den), pdup(cp.lg2_floor));
+        const f2 G = pmed3(f2{fast_exp2(e.x), fast_exp2(e.y)}, cp.gclip, 1.0f);
+        rr = (G * G) * gam;
+        return G;
+    }
+}
+
+// One frame's gain stage + real-IFFT packing for one lane, packed (CSE_PK,
+// pair-order rows): per mirror pair the gains of both bins (gain_pair; SS per
+// bin through gain_bin), then
+//   X_k = Y_k g_k,  conj(X_{M-k}) = Y_{M-k} (g', -g'),  g' = g_{M-k}
+//   S = X_k + conj(X_{M-k}),  D = X_k - conj(X_{M-k}),  P = D w
+//   Z'[k] = S + i P,  Z'[M - k] = conj(S) + i conj(P)
+// (8 packed instructions per pair).  z[j] keeps Z'[k]; xw[j] goes to the
+// mirror lane.  Bin M/2 (the 17th item) stays scalar (gain_bin).  Rows: Y
+// records (Y_p, Y_{M-p}) (16 B); at 512 (g_p, g_{M-p}, d_p, d_{M-p}) (16 B) and
+// MMSE's / SS's a pairs (8 B), at 1024 (g_p, g_{M-p}) (8 B).  Packing rotors:
+// the lane's table row (512) or base x W32^j (1024).
+template <int NFFT, int ALGO, bool OUT>
+__device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
+                                             const void* __restrict__ growv,
+                                             const float2* __restrict__ a2row, f2 (&z)[16],
+                                             f2* __restrict__ xw, f2 (&rr)[8], float& rrm,
+                                             float alpha_t, const CellParam& cpar,
+                                             const float4* __restrict__ rot4,
+                                             const cf* __restrict__ base_p,
+                                             float* __restrict__ gout_row, int i) {
+    constexpr int L = Geo<NFFT>::L, M = Geo<NFFT>::M;
+    constexpr bool R2 = (NFFT == 512);
+    constexpr bool WANT_A = R2 && (ALGO == CSE_ALGO_MMSE || (ALGO == CSE_ALGO_SS && OUT));
+    const float4* y4 = y4row + i;
+    const float4* g4 = (const float4*)growv + i;  // 512
+    const float2* g2 = (const float2*)growv + i;  // 1024
+    const float2* a2 = a2row + i;
+    // (gamma pair, d pair) of a record: d unused at 1024
+    auto ldg = [&](int k) {
+        if constexpr (R2) return g4[k];
+        const float2 v = g2[k];
+        return make_float4(v.x, v.y, 0.0f, 0.0f);
+    };
+    float4 yc = y4[0], gc = ldg(0);
+    float2 ac = WANT_A ? a2[0] : make_float2(0.0f, 0.0f);
+    const cf base = R2 ? cmk(1.0f, 0.0f) : *base_p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        // next pair's rows (j = 7: bin M/2, the record of pair M/2)
+        const int nx = (j < 7) ? L * (j + 1) : M / 2 - i;
+        const float4 yn = y4[nx], gn = ldg(nx);
+        const float2 an = WANT_A ? a2[nx] : make_float2(0.0f, 0.0f);
+        f2 ya = f2{yc.x, yc.y}, yb = f2{yc.z, yc.w};
+        f2 g;  // the pair's gains
+        f2 s;  // the real factors of S = Y s (SS: sqrt(Ps) on the unit phasor)
+        if (ALGO == CSE_ALGO_SS) {
+            float2 y0 = make_float2(ya.x, ya.y), y1 = make_float2(yb.x, yb.y);
+            float g0, g1, dummy = 0.0f;
+            const float s0 = gain_bin<NFFT, ALGO>(y0, RowV{gc.x, gc.z, ac.x}, dummy, alpha_t, cpar, g0);
+            const float s1 = gain_bin<NFFT, ALGO>(y1, RowV{gc.y, gc.w, ac.y}, dummy, alpha_t, cpar, g1);
+            g = f2{g0, g1};
+            s = f2{s0, s1};
+            ya = f2{y0.x, y0.y};  // 1024: the rescaled phasor source where Y is tiny
+            yb = f2{y1.x, y1.y};
+        } else {
+            g = gain_pair<NFFT, ALGO>(f2{gc.x, gc.y}, f2{gc.z, gc.w}, f2{ac.x, ac.y}, rr[j], alpha_t, cpar);
+            s = g;
+        }
+        if (OUT && gout_row) {
+            gout_row[i + L * j] = g.x;
+            gout_row[M - i - L * j] = g.y;
+        }
+        if (j == 0 && i == 0) {  // irfft ignores Im of DC and Nyquist
+            ya.y = 0.0f;
+            yb.y = 0.0f;
+        }
+        const f2 xk = ya * s.xx;
+        const f2 S = p_fma_conj_hi(yb, s, xk), D = p_fms_conj_hi(yb, s, xk);
+        f2 w;
+        if constexpr (R2) {
+            const float4 q4 = rot4[j >> 1];  // two packing rotors
+            w = (j & 1) ? f2{q4.z, q4.w} : f2{q4.x, q4.y};
+        } else {
+            // base x W32^j in scalar form (instruction literals, no SGPR pairs)
+            const cf wj = (j == 0) ? base : cmul(base, cmk(Rot32::c[j], Rot32::s[j]));
+            w = f2{wj.x, wj.y};
+        }
+        const f2 P = p_cmul(D, w);
+        z[j] = p_addi(S, P);                      // Z'[k] = S + i P
+        xw[j] = p_conj_addi(S, P);                // Z'[M - k] = conj(S) + i conj(P)
+        yc = yn;
+        gc = gn;
+        ac = an;
+    }
+    // bin M/2: scalar, Z'[M/2] = 2 conj(X_{M/2})
+    float2 ym = make_float2(yc.x, yc.y);
+    float gm;
+    const float sm = 2.0f * gain_bin<NFFT, ALGO>(ym, RowV{gc.x, gc.z, ac.x}, rrm, alpha_t, cpar, gm);
+    if (OUT && gout_row && i == 0) gout_row[M / 2] = gm;
+    xw[8] = f2{ym.x * sm, -ym.y * sm};
 }
 
 // One frame's gain stage + real-IFFT packing for one lane.
@@ -638,10 +821,25 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 if (k < B) {
                     const float2 y = py[u];
                     const float P = y.x * y.x + y.y * y.y;
+                    // pair order (CSE_PK): bin k goes to half h of mirror pair p,
+                    // the 16-B records (Y_p, Y_{M-p}) and (g_p, g_{M-p}, d_p, d_{M-p})
+                    const int pp = k <= M / 2 ? k : M - k, hh = k <= M / 2 ? 0 : 1;
+                    auto put = [&](float2 yv, float gv, float dv) {
+                        if constexpr (W::PK) {
+                            yrow[2 * pp + hh] = yv;
+                            grow[4 * pp + hh] = gv;
+                            grow[4 * pp + 2 + hh] = dv;
+                        } else {
+                            yrow[k] = yv;
+                            grow2[k] = make_float2(gv, dv);
+                        }
+                    };
+                    const int ai = W::PK ? 2 * pp + hh : k;
                     if (!W::R2) {
-                        yrow[k] = y;
                         const float gam = fmaxf(P * pn[u], EPS);
-                        grow[k] = (ALGO == CSE_ALGO_SS) ? pn[u] : (ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam);
+                        const float gv = (ALGO == CSE_ALGO_SS) ? pn[u] : (ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam);
+                        yrow[W::PK ? 2 * pp + hh : k] = y;  // pair order: 8-B gamma records
+                        grow[W::PK ? 2 * pp + hh : k] = gv;
                     } else if (ALGO == CSE_ALGO_SS) {
                         // phasor y/|y| of the y rescaled by 2^64 below 2^-50
                         // (v_rsq flushes denormals); (1, 0) where y = 0
@@ -649,17 +847,14 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                         const float yx = y.x * sc, yy = y.y * sc;
                         const float pz = fmaf(yx, yx, yy * yy);
                         const float r = __builtin_amdgcn_rsqf(pz);
-                        yrow[k] = pz > 0.0f ? make_float2(yx * r, yy * r) : make_float2(1.0f, 0.0f);
-                        grow2[k] = make_float2(pn[u], P);
-                        if (OUT) arow[k] = pz > 0.0f ? r * sc : 0.0f;
+                        put(pz > 0.0f ? make_float2(yx * r, yy * r) : make_float2(1.0f, 0.0f), pn[u], P);
+                        if (OUT) arow[ai] = pz > 0.0f ? r * sc : 0.0f;
                     } else {
-                        yrow[k] = y;
                         const float gam = fmaxf(P * pn[u], EPS);
                         // OMLSA's bins take gamma log2(e) (gain_omlsa), d from gamma
-                        grow2[k] = make_float2(ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam,
-                                               fmaxf(gam - 1.0f, 0.0f));
+                        put(y, ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam, fmaxf(gam - 1.0f, 0.0f));
                         if (ALGO == CSE_ALGO_MMSE)
-                            arow[k] = 0.88622692545275801f * fast_rcp(gam + 1e-12f);
+                            arow[ai] = 0.88622692545275801f * fast_rcp(gam + 1e-12f);
                     }
                 }
             }
@@ -689,14 +884,22 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     float rr[17];  // prev_gain**2 * prev_gamma per bin (read from frame 1 on)
 #pragma unroll
     for (int j = 0; j < 17; ++j) rr[j] = 0.0f;
+    f2 rr2[8];       // CSE_PK: the same state per mirror pair (k, M - k) ...
+    float rrm = 0.0f;  // ... and of bin M/2
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rr2[j] = f2{0.0f, 0.0f};
     float acc[PEND];  // overlap-add sums of the positions frame t's slots q < PEND cover
 #pragma unroll
     for (int q = 0; q < PEND; ++q) acc[q] = 0.0f;
+    f2 acc2[PEND / 2];  // CSE_PK: the same sums in slot pairs (q, q + 1)
+#pragma unroll
+    for (int q = 0; q < PEND / 2; ++q) acc2[q] = f2{0.0f, 0.0f};
     double sse = 0.0;
     float chk = 0.0f;  // sum of y*0 over retired samples: NaN iff some y is not finite
 
     for (int t = 0; t < nf + R - 1; ++t) {
         float x[32];  // this frame's windowed IFFT samples (0 in flush frames)
+        f2 xp[16];    // CSE_PK: the same as pairs (x[2p], x[2p + 1])
         // the lane's window slots: ds_read_b128 from its 16-B aligned table row
         // (issued before the pass-2 DFT instead: +0.7 % at 512, the 32 VGPRs
         // held through it cost more than the latency they hide)
@@ -713,7 +916,101 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             }
         };
 
-        if (t < nf) {
+        if (W::PK && t < nf) {
+            // the frame in packed pairs (CSE_PK; same stages as the branch below)
+            __syncthreads();
+            CSE_MARK("gain");
+            __builtin_amdgcn_s_setprio(1);
+            f2 z[16];
+            {
+                const CellParam cpar = *(const CellParam*)(smem + W::OFF_CP + 32 * cslot);
+                const float alpha_t = (t == 0) ? 0.0f : cpar.p0;
+                const int yb = W::OFF_Y + (t & 1) * W::YROW, gb = W::OFF_G + (t & 1) * W::GROW;
+                const int ab = W::OFF_A + (t & 1) * W::AROW;
+                gain_pack_pk<NFFT, ALGO, OUT>((const float4*)(smem + yb), (const void*)(smem + gb),
+                                              (const float2*)(smem + ab), z, (f2*)(smem + creg + 72 * i),
+                                              rr2, rrm, alpha_t, cpar,
+                                              (const float4*)(smem + W::OFF_LC + W::ROTSTR * i),
+                                              (const cf*)(smem + W::OFF_LC + 8 * i),
+                                              (OUT && gout) ? gout + t * B : nullptr, i);
+            }
+            __builtin_amdgcn_s_setprio(0);
+            CSE_MARK("xchg");
+            wave_sync();
+            {
+                const int partner = (L - i) & (L - 1);
+                const f2* xr = (const f2*)(smem + creg + 72 * partner + (i == 0 ? 8 : 0));
+#pragma unroll
+                for (int s = 8; s < 16; ++s) z[s] = xr[15 - s];
+            }
+            CSE_MARK("rows");
+            store_rows(t + 1);
+            load_rows(t + 2);
+            CSE_MARK("pass1");
+            if constexpr (W::ROTOR_TW) {  // see the scalar branch
+                const float4* q4 = (const float4*)(smem + W::OFF_TW + 48 * i);
+                const float4 qa = q4[0], qb = q4[1], qc = q4[2];
+                idft16_pk(z);
+                const f2 lo[4] = {f2{1.0f, 0.0f}, f2{qa.x, qa.y}, f2{qa.z, qa.w}, f2{qb.x, qb.y}};
+                const f2 hi[4] = {f2{1.0f, 0.0f}, f2{qb.z, qb.w}, f2{qc.x, qc.y}, f2{qc.z, qc.w}};
+#pragma unroll
+                for (int b = 1; b < 16; ++b) {
+                    const f2 tb = (b & 3) == 0 ? hi[b >> 2] : (b < 4 ? lo[b] : p_cmul(lo[b & 3], hi[b >> 2]));
+                    z[b] = p_cmul(z[b], tb);
+                }
+            } else {
+                const float4* twr = (const float4*)(smem + W::OFF_TW + 144 * i);
+#if CSE_JIT_TABLES  // each twiddle pair read right before its products
+                idft16_pk(z);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float4 q4 = twr[k];
+                    z[2 * k + 1] = p_cmul(z[2 * k + 1], f2{q4.x, q4.y});
+                    if (k < 7) z[2 * k + 2] = p_cmul(z[2 * k + 2], f2{q4.z, q4.w});
+                }
+#else
+                float4 t4[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) t4[k] = twr[k];
+                idft16_pk(z);
+#pragma unroll
+                for (int b = 1; b < 16; ++b) {
+                    const float4 q4 = t4[(b - 1) >> 1];
+                    z[b] = p_cmul(z[b], ((b - 1) & 1) ? f2{q4.z, q4.w} : f2{q4.x, q4.y});
+                }
+#endif
+            }
+            CSE_MARK("pass2");
+            f2 v[16];
+            {
+                constexpr int TS = W::TS;
+                wave_sync();
+                f2* tw_ = (f2*)(smem + creg + 8 * i);
+                const f2* tr = (const f2*)(smem + creg + 8 * TS * b2);
+#pragma unroll
+                for (int b = 0; b < 16; ++b) tw_[b * TS] = z[b];
+                wave_sync();
+                if constexpr (L == 32) {  // DFT32: radix-2 on the read side, see the scalar branch
+                    const float sg = h2 ? -1.0f : 1.0f;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const f2 u = pfma(pdup(sg), tr[r + 16], tr[r]);
+                        // the rotor product in scalar form: its constants are
+                        // instruction literals (16 packed rotor pairs would take
+                        // 64 SGPRs, and the kernel spilled 192)
+                        const cf ur = cmul(cmk(u.x, u.y), cmk(Rot32::c[r], Rot32::s[r]));
+                        v[r] = h2 ? f2{ur.x, ur.y} : u;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) v[r] = tr[r];
+                }
+            }
+            idft16_pk(v);
+            CSE_MARK("window");
+#pragma unroll
+            for (int p = 0; p < 16; ++p) xp[p] = v[p];
+        } else if (t < nf) {
             // the one workgroup barrier per frame: rows(t) (stored during frame
             // t-1) are visible, and nobody still reads buffer (t+1)&1
             __syncthreads();
@@ -839,6 +1136,8 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             load_rows(t + 2);
 #pragma unroll
             for (int q = 0; q < 32; ++q) x[q] = 0.0f;
+#pragma unroll
+            for (int p = 0; p < 16; ++p) xp[p] = f2{0.0f, 0.0f};
         }
 
         CSE_MARK("retire");
@@ -858,10 +1157,26 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             return (W::HALF_TABLES && q >= 16) ? KHALF - wv[q - 16] : wv[q];
         };
         float done[F];
+        f2 done2[F / 2];
+        if constexpr (W::PK) {  // slot pairs (q, q + 1) = (Re, Im) of one IFFT output
 #pragma unroll
-        for (int q = 0; q < F; ++q) done[q] = fmaf(x[q], win(q), acc[q]);
+            for (int p = 0; p < F / 2; ++p) {
+                done2[p] = pfma(xp[p], f2{win(2 * p), win(2 * p + 1)}, acc2[p]);
+                done[2 * p] = done2[p].x;
+                done[2 * p + 1] = done2[p].y;
+            }
 #pragma unroll
-        for (int q = 0; q < PEND; ++q) acc[q] = fmaf(x[q + F], win(q + F), q + F < PEND ? acc[q + F] : 0.0f);
+            for (int p = 0; p < PEND / 2; ++p) {
+                const int q = 2 * p + F;
+                acc2[p] = pfma(xp[q / 2], f2{win(q), win(q + 1)},
+                               q < PEND ? acc2[p + F / 2] : f2{0.0f, 0.0f});
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < F; ++q) done[q] = fmaf(x[q], win(q), acc[q]);
+#pragma unroll
+            for (int q = 0; q < PEND; ++q) acc[q] = fmaf(x[q + F], win(q + F), q + F < PEND ? acc[q + F] : 0.0f);
+        }
         if (valid) {
             const int o0 = t * HOP + off - NFFT / 2;  // output index of q = 0
             const float* crow_t = (const float*)__builtin_assume_aligned(
@@ -884,8 +1199,25 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 #pragma unroll
                 for (int k = 0; k < F / 2; ++k) cl2[k] = *(const float2*)(crow_t + SP * k);
                 float pa = 0.0f, pb = 0.0f, ca = 0.0f, cb = 0.0f;
+                if constexpr (W::PK) {  // the two chains as one pair
+                    f2 pp = f2{0.0f, 0.0f}, cc = f2{0.0f, 0.0f};
 #pragma unroll
-                for (int q = 0; q < F; ++q) {
+                    for (int p = 0; p < F / 2; ++p) {
+                        const f2 y = done2[p];
+                        const int n = SP * p;
+                        if (head && yout && o0 + n < out_len) yout[o0 + n] = y.x;
+                        if (head && yout && o0 + n + 1 < out_len) yout[o0 + n + 1] = y.y;
+                        const f2 d = f2{cl2[p].x, cl2[p].y} - pmed3(y, -1.0f, 1.0f);
+                        cc = pfma(y, pdup(0.0f), cc);
+                        pp = pfma(d, d, pp);
+                    }
+                    pa = pp.x;
+                    pb = pp.y;
+                    ca = cc.x;
+                    cb = cc.y;
+                }
+#pragma unroll
+                for (int q = 0; q < (W::PK ? 0 : F); ++q) {
                     const int n = SP * (q >> 1) + (q & 1);
                     const float y = done[q];
                     if (head && yout && o0 + n < out_len) yout[o0 + n] = y;

@@ -40,24 +40,35 @@ constexpr int XT = 256;       // threads per workgroup
 constexpr int XCAND = 64;     // more fp64 candidates than this: status FLAT
 constexpr int XLAGS = 2 * ((XN - XB) / 2) + 1;  // most lags a cell has (max_lag <= 1600)
 constexpr int XWORDS = (XLAGS + 31) / 32;        // candidate bitmap words
-constexpr int XHP = XH + XH / 16;  // LDS FFT buffer, one pad slot after every 16 points
-// padded LDS index: the first Stockham pass stores 16 consecutive points per
-// lane (lane stride 16 x 8 B, a 32-way bank conflict unpadded; 17 x 8 B with
-// the pad), every other access runs over consecutive points
-__device__ __forceinline__ int px(int p) { return p + (p >> 4); }
+constexpr int XHP = XH + XH / 16;  // LDS FFT buffer (room for the 1-in-16 padded layout)
+// Two padded LDS layouts of the 4096 points.  px16 (one pad slot after every
+// 16 points) is what the first Stockham pass stores: 16 consecutive points per
+// lane, lane stride 17 x 8 B, so the 16 lanes of a ds_write_b64 group hit
+// distinct banks (unpadded: a 32-way conflict).  Every other access runs over
+// consecutive points, 32 lanes per ds_read_b64 group, and there px16's pad
+// wraps the group's last lane onto its first lane's banks (a 2-way conflict on
+// every read: r03's 1.16 conflict cycles per LDS instruction); px32 (one pad
+// slot per 32 points) keeps such a group contiguous.  The passes convert: the
+// first pass reads px32 and writes px16, the second reads px16 and writes
+// px32, everything else is px32.
+template <int PAD>
+__device__ __forceinline__ int pxl(int p) { return p + (PAD == 16 ? (p >> 4) : (p >> 5)); }
+__device__ __forceinline__ int px(int p) { return pxl<32>(p); }
+constexpr int XR = XH / 16 + XH / 16 / 32;  // px32 stride of 256 points: 264
 #ifndef CSE_XC_WG_PER_CU
 #define CSE_XC_WG_PER_CU 3    // 168 VGPRs + 72 B spill: 4% faster than 2 (192, no spill); 4 spills 240 B
 #endif
 
 // one radix-16 Stockham pass of stride NS (compile-time, so every padded
-// address is a constant offset from one per-lane base)
-template <int DIR, int NS>
+// address is a constant offset from one per-lane base), reading layout PI and
+// writing layout PO
+template <int DIR, int NS, int PI, int PO>
 __device__ __forceinline__ void fft4096_pass(cf* buf) {
     const int j = threadIdx.x;
     cf v[16];
-    const int pj = px(j);  // point j + 256 r sits at pj + 272 r
+    const int pj = pxl<PI>(j);  // point j + 256 r sits at pj + (256 + 256/PI) r
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = buf[pj + r * (XH / 16 + XH / 256)];
+    for (int r = 0; r < 16; ++r) v[r] = buf[pj + r * (XH / 16 + XH / 16 / PI)];
     const int k = j % NS;
     if (NS > 1) {
         // w^r, w = e^{DIR 2πi k/(16 NS)}: one accurate sincos, then a product
@@ -85,13 +96,12 @@ __device__ __forceinline__ void fft4096_pass(cf* buf) {
         for (int r = 0; r < 16; ++r) v[r].y = -v[r].y;
     }
     __syncthreads();
-    // px(base + r NS) = px(base) + r (NS + NS / 16) for NS >= 16 (base + r NS never
-    // carries into the pad index); NS = 1: base = 16 j, px = 17 j + r
+    // pxl(base + r NS) = pxl(base) + r NS + (r NS) / PO: base's low part (k < NS,
+    // or base = 16 j at NS = 1) never carries into the pad index
     const int base = (j / NS) * NS * 16 + k;
-    const int pb = px(base);
-    constexpr int PS = NS == 1 ? 1 : NS + NS / 16;
+    const int pb = pxl<PO>(base);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) buf[pb + r * PS] = v[r];
+    for (int r = 0; r < 16; ++r) buf[pb + r * NS + (r * NS) / PO] = v[r];
     __syncthreads();
 }
 
@@ -99,9 +109,9 @@ __device__ __forceinline__ void fft4096_pass(cf* buf) {
 // radix-16 Stockham (Govindaraju et al. 2008 form): 3 passes, natural order out
 template <int DIR>
 __device__ __forceinline__ void fft4096(cf* buf) {
-    fft4096_pass<DIR, 1>(buf);
-    fft4096_pass<DIR, 16>(buf);
-    fft4096_pass<DIR, 256>(buf);
+    fft4096_pass<DIR, 1, 32, 16>(buf);
+    fft4096_pass<DIR, 16, 16, 32>(buf);
+    fft4096_pass<DIR, 256, 32, 32>(buf);
 }
 
 // X(f), f = 0..XH, of the real sequence x[2m] + i x[2m+1] = buf[m] after fft4096<-1>:
@@ -126,10 +136,10 @@ __device__ __forceinline__ cf rfft_pair(cf z, cf w, cf tw) {
 
 // padded LDS index of the mirror (XH - f) mod XH of the lane's bin f = t + 256 r:
 // t > 0: (256 - t) + 256 (15 - r); t = 0: 256 (16 - r) mod XH.  mirror_base(t)
-// + 272 (15 - r) covers both, except (t, r) = (0, 0) -> 0 (see mirror_at)
-__device__ __forceinline__ int mirror_base(int t) { return t == 0 ? 272 : px(256 - t); }
+// + XR (15 - r) covers both, except (t, r) = (0, 0) -> 0 (see mirror_at)
+__device__ __forceinline__ int mirror_base(int t) { return t == 0 ? XR : px(256 - t); }
 __device__ __forceinline__ int mirror_at(int mb, int t, int r) {
-    const int q = mb + 272 * (15 - r);
+    const int q = mb + XR * (15 - r);
     return r == 0 ? (t == 0 ? 0 : q) : q;
 }
 
@@ -332,14 +342,19 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     const float* e = a.head + a.head_offset[cell];
     const int n = a.n, L = a.max_lag;
 
-    // C(f) = sum_b R_b(f) conj(S_b(f)); thread owns f = tid + XT r (+ f = XH on thread 0).
-    // The blocks tile e[0, n) exactly once, so the mean and energy of e are
-    // accumulated from the same loads (all 32 of a block's samples per lane are
-    // issued before the first is used: one memory latency per block, not 16).
-    cf C[16];
-    cf Cn = cmk(0.0f, 0.0f);
+    // C(f) = sum_b R_b(f) conj(S_b(f)).  Thread t owns the mirror pairs (f, XH - f),
+    // f = t + XT r, r < 8 (f = 0 pairs with the Nyquist bin XH), thread 0 also
+    // f = XH/2 (its own mirror): both bins of a pair come from the same two FFT
+    // points, X(f) = E + w O and X(XH - f) = conj(E - w O) (w = e^{-2πi f/XN}),
+    // so each point is read once, and the inverse transform's packing needs no
+    // exchange either.  The blocks tile e[0, n) exactly once, so the mean and
+    // energy of e are accumulated from the same loads (all 20 of a block's
+    // samples per lane are issued before the first is used: one memory latency
+    // per block, not 16).
+    cf C[8], Cm[8];  // C(f), C(XH - f)
+    cf Ch = cmk(0.0f, 0.0f);  // C(XH/2), thread 0
 #pragma unroll
-    for (int r = 0; r < 16; ++r) C[r] = cmk(0.0f, 0.0f);
+    for (int r = 0; r < 8; ++r) C[r] = Cm[r] = cmk(0.0f, 0.0f);
     double s1 = 0.0, s2 = 0.0;
     const float2* Rs = a.R + (int64_t)sig * a.nb * (XH + 1);
     const cf rot_tid = bin_rotor(tid);
@@ -380,30 +395,39 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-            buf[pt + 272 * r] = r < 10 ? cmk(x[2 * r], x[2 * r + 1]) : cmk(0.0f, 0.0f);
-        // R_b is issued before the transform and consumed after it
+            buf[pt + XR * r] = r < 10 ? cmk(x[2 * r], x[2 * r + 1]) : cmk(0.0f, 0.0f);
+        // R_b at the lane's bins is issued before the transform and consumed after it
         const float2* Rb = Rs + (int64_t)b * (XH + 1);
-        float2 rr[16];
+        float2 rr[8], rm[8];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) rr[r] = Rb[tid + XT * r];
+        for (int r = 0; r < 8; ++r) {
+            rr[r] = Rb[tid + XT * r];
+            rm[r] = Rb[XH - tid - XT * r];  // thread 0, r = 0: the Nyquist bin
+        }
+        const float2 rh = Rb[XH / 2];
         __syncthreads();
         fft4096<-1>(buf);
-        cf rt = rot_tid;  // hidden: the 16 derived rotors must not live across the FFT
+        cf rt = rot_tid;  // hidden: the 8 derived rotors must not live across the FFT
         asm volatile("" : "+v"(rt.x), "+v"(rt.y));
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
+        for (int r = 0; r < 8; ++r) {
             // e^{-2πi (tid + 256 r)/8192} = rot_tid * e^{-2πi r/32}
-            const cf s = rfft_pair(buf[pt + 272 * r], buf[mirror_at(mb, tid, r)],
-                                   cmul(rt, cmk(Rot32::c[r], -Rot32::s[r])));
+            const cf z = buf[pt + XR * r], w = buf[mirror_at(mb, tid, r)];
+            const cf e = cmk(0.5f * (z.x + w.x), 0.5f * (z.y - w.y));
+            const cf o = cmk(0.5f * (z.y + w.y), -0.5f * (z.x - w.x));
+            const cf wo = cmul(cmul(rt, cmk(Rot32::c[r], -Rot32::s[r])), o);
+            const cf sf = cadd(e, wo);                      // X(f)
+            const cf sg = cmk(e.x - wo.x, wo.y - e.y);      // X(XH - f) = conj(E - w O)
             // R conj(S)
-            C[r].x += rr[r].x * s.x + rr[r].y * s.y;
-            C[r].y += rr[r].y * s.x - rr[r].x * s.y;
+            C[r].x += rr[r].x * sf.x + rr[r].y * sf.y;
+            C[r].y += rr[r].y * sf.x - rr[r].x * sf.y;
+            Cm[r].x += rm[r].x * sg.x + rm[r].y * sg.y;
+            Cm[r].y += rm[r].y * sg.x - rm[r].x * sg.y;
         }
-        if (tid == 0) {
-            const cf s = rfft_bin(buf, XH, cmk(1.0f, 0.0f));
-            const float2 rr = Rb[XH];
-            Cn.x += rr.x * s.x + rr.y * s.y;
-            Cn.y += rr.y * s.x - rr.x * s.y;
+        if (tid == 0) {  // X(XH/2) = conj(Z_{XH/2})
+            const cf z = buf[px(XH / 2)];
+            Ch.x += rh.x * z.x - rh.y * z.y;
+            Ch.y += rh.y * z.x + rh.x * z.y;
         }
         __syncthreads();
     }
@@ -429,26 +453,20 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
         }
         return;
     }
-    // inverse real transform: Zi(f) = (C_f + conj C_{XH-f}) + i e^{+2πi f/XN} (C_f - conj C_{XH-f})
+    // inverse real transform: Zi(f) = (C_f + conj C_{XH-f}) + i e^{+2πi f/XN} (C_f - conj C_{XH-f});
+    // with ev, od those two terms, Zi(XH - f) = conj(ev - i t), t = e^{+2πi f/XN} od,
+    // and Zi(XH/2) = 2 conj(C_{XH/2}): every point from the lane's own pairs
 #pragma unroll
-    for (int r = 0; r < 16; ++r) buf[pt + 272 * r] = C[r];
-    __shared__ cf cnyq;
-    if (tid == 0) cnyq = Cn;
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int f = tid + XT * r;
-        const cf cf_ = C[r];
-        const cf cm = (f == 0) ? cnyq : buf[mirror_at(mb, tid, r)];
-        const cf ev = cmk(cf_.x + cm.x, cf_.y - cm.y);
-        const cf od = cmk(cf_.x - cm.x, cf_.y + cm.y);
+    for (int r = 0; r < 8; ++r) {
+        const cf ev = cmk(C[r].x + Cm[r].x, C[r].y - Cm[r].y);
+        const cf od = cmk(C[r].x - Cm[r].x, C[r].y + Cm[r].y);
         const cf tw = cmul(rot_tid, cmk(Rot32::c[r], -Rot32::s[r]));  // e^{-2πi f/XN}
         const cf t = cmul(cmk(tw.x, -tw.y), od);                       // e^{+2πi f/XN} od
-        C[r] = cmk(ev.x - t.y, ev.y + t.x);  // ev + i t
+        buf[pt + XR * r] = cmk(ev.x - t.y, ev.y + t.x);                // ev + i t
+        if (r > 0 || tid > 0)  // f = 0: its mirror is XH, not an input point
+            buf[mirror_at(mb, tid, r)] = cmk(ev.x + t.y, t.x - ev.y);  // conj(ev - i t)
     }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) buf[pt + 272 * r] = C[r];
+    if (tid == 0) buf[px(XH / 2)] = cmk(2.0f * Ch.x, -2.0f * Ch.y);
     __syncthreads();
     fft4096<1>(buf);
 

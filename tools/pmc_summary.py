@@ -37,16 +37,24 @@ def stats(path):
 
 
 def counters(pattern, kname):
-    """{counter: value per launch} over the matching dispatches of all pmc dirs."""
-    acc, disp = {}, {}
-    for f in glob.glob(pattern):
+    """{counter: value per launch} over the matching dispatches of all pmc dirs:
+    per pass (file) the sum over its dispatches / its dispatches, and a counter
+    that several passes collected (GRBM_GUI_ACTIVE, SQ_INSTS_VALU, ...) is the
+    mean of their per-launch values (r03's summaries summed such counters over
+    the passes, e.g. GRBM_GUI_ACTIVE twice)."""
+    per, disp = {}, {}
+    for f in sorted(glob.glob(pattern)):
+        acc, dd = {}, {}
         for r in csv.DictReader(open(f)):
             if kname not in r["Kernel_Name"]:
                 continue
             c = r["Counter_Name"]
             acc[c] = acc.get(c, 0.0) + float(r["Counter_Value"])
-            disp.setdefault(c, set()).add(r["Dispatch_Id"])
-    return {c: v / len(disp[c]) for c, v in acc.items()}, {c: len(d) for c, d in disp.items()}
+            dd.setdefault(c, set()).add(r["Dispatch_Id"])
+        for c, v in acc.items():
+            per.setdefault(c, []).append(v / len(dd[c]))
+            disp[c] = disp.get(c, 0) + len(dd[c])
+    return {c: sum(v) / len(v) for c, v in per.items()}, disp
 
 
 def derive(pmc, kernel_ms):
@@ -102,6 +110,27 @@ def main(tag, rnd, units512=None, units1024=None):
         pmc, nd = counters(os.path.join(base, f"pmc_{pmcname}_*", "run_counter_collection.csv"), kname)
         summary["kernels"][key] = {"kernel": kname, "kernel_ms_rocprof": ms, "pmc_per_launch": pmc,
                                    "pmc_launches": nd, **derive(pmc, ms)}
+    # r04: the n_fft 512 kernel issues packed f32 (v_pk_*) instructions, two f32
+    # operations each, which SQ_INSTS_VALU counts once.  Its VALU issue cycles are
+    # therefore taken from the scalar build of the same sources (CSE_PK=0: every
+    # f32 operation its own instruction, pmc_s512_*), over the product build's
+    # own busy cycles; both builds' SQPK passes (pk512, s512_pk) are recorded.
+    k512 = summary["kernels"]["enhance512"]
+    spmc, _ = counters(os.path.join(base, "pmc_s512_sq1", "run_counter_collection.csv"), KERNELS["enhance512"])
+    spk, _ = counters(os.path.join(base, "pmc_s512_pk", "run_counter_collection.csv"), KERNELS["enhance512"])
+    ppk, _ = counters(os.path.join(base, "pmc_pk512", "run_counter_collection.csv"), KERNELS["enhance512"])
+    if spmc:
+        k512["pmc_scalar_build_per_launch"] = spmc
+        k512["pmc_scalar_build_pk_pass_per_launch"] = spk
+        k512["pmc_packed_counters_per_launch"] = ppk
+        sd = derive(spmc, None)
+        busy = k512["pmc_per_launch"].get("SQ_BUSY_CYCLES")
+        if sd.get("valu_issue_cycles") and busy:
+            k512["valu_issue_cycles_own_count"] = k512.get("valu_issue_cycles")
+            k512["valu_issue_cycles"] = sd["valu_issue_cycles"]
+            k512["valu_frac"] = sd["valu_issue_cycles"] / (SIMDS * busy / 32)
+            k512["valu_issue_cycles_source"] = ("scalar build (CSE_PK=0) instruction counts: a packed f32 "
+                                                "instruction does the work of two scalar ones")
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
     json.dump(summary, open(os.path.join(REPO, "profiles", f"{rnd}_kernels.json"), "w"), indent=1)
     for key, units in (("enhance512", units512), ("enhance1024", units1024)):
@@ -117,6 +146,7 @@ def main(tag, rnd, units512=None, units1024=None):
                "sq_busy_cycles": pmc.get("SQ_BUSY_CYCLES"),
                "valu_frac": k.get("valu_frac"), "clock_ghz_profiled": k.get("clock_ghz_profiled"),
                "valu_issue_cycles": k.get("valu_issue_cycles"),
+               "valu_issue_cycles_source": k.get("valu_issue_cycles_source", "this build's counts"),
                "share_wait_inst_any": k.get("share_wait_inst_any"),
                "lds_conflict_cycles_per_lds_inst": k.get("lds_conflict_cycles_per_lds_inst"),
                "kernel_src_sha": src_sha,

@@ -4,12 +4,12 @@
 #   enhance_kernel<512>  : bench.py (BASELINE config 4 job, 100 pairs) -- the bench line
 #   enhance_kernel<1024> : bench.py --nfft 1024
 #   stoi_cells_kernel, xcorr_*: tools/bench_sweep.py (full grid, 4 pairs)
-#     bash tools/profile_all.sh TAG [what...]     what in {kt512, kt1024, ktsweep, pmc512, pmc1024, pmcstoi}
+#     bash tools/profile_all.sh TAG [what...]     what in {kt512, kt1024, ktsweep, pmc512, pmc1024, pmcstoi, pmcpk, pmc512s}
 # Output under gpurun_out/prof_TAG/; tools/pmc_summary.py turns it into profiles/*.json.
 set -o pipefail
 TAG=${1:-dev}
 shift
-WHAT=${*:-kt512 kt1024 ktsweep pmc512 pmc1024 pmcstoi}
+WHAT=${*:-kt512 kt1024 ktsweep pmc512 pmc1024 pmcstoi pmcpk pmc512s}
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
@@ -22,6 +22,11 @@ SWEEP="tools/bench_sweep.py --pairs 4 --reps 1"
 SQ1="SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
 SQ2="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"
 SQF64="SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+# r04: how the counters see packed f32 (v_pk_*) instructions
+SQPK="SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_FLOPS_FP32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+# the scalar build of the same sources (CSE_PK=0): the VALU issue cycles of
+# the arithmetic with every f32 operation its own instruction
+SCALAR_LIB=${SCALAR_LIB:-classical_speech_enhancement_amd/libcse_scalar.so}
 
 kt() {  # name, command...
   local name=$1; shift
@@ -44,6 +49,8 @@ for w in $WHAT; do
     pmc1024) pmc 1024_fetch FETCH_SIZE $P1024 && pmc 1024_write WRITE_SIZE $P1024 &&
              pmc 1024_sq1 "$SQ1" $P1024 && pmc 1024_sq2 "$SQ2" $P1024 ;;
     pmcstoi) pmc stoi_f64 "$SQF64" $SWEEP && pmc stoi_sq2 "$SQ2" $SWEEP ;;
+    pmcpk) pmc pk512 "$SQPK" $P512 ;;
+    pmc512s) CSE_LIB=$SCALAR_LIB pmc s512_sq1 "$SQ1" $P512 && CSE_LIB=$SCALAR_LIB pmc s512_pk "$SQPK" $P512 ;;
     *) echo "unknown $w"; exit 1 ;;
   esac
 done
