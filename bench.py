@@ -55,6 +55,7 @@ sys.path.insert(0, REPO)
 METRIC = ("STFT frame-gain evals/sec/node, 16kHz 512-pt FFT full grid; 1/2/4/8-GPU scaling")
 HBM_PEAK = 8.0e12              # MI355X_MICROARCH.md: 8.0 TB/s spec
 SIMDS = 1024                   # 256 CUs x 4 SIMD-32
+DENSE_VALU_CYC, DENSE_TRANS_CYC = 2.71, 4.86  # tools/micro/valu_peak.hip, 8 waves/SIMD
 VALU_CYC, TRANS_CYC = 2, 4     # wave64 issue cycles: v_fma_f32 (SIMD-32), transcendental (2x: tools/micro/valu_rate.hip)
 CLOCK = 2.4e9                  # max shader clock
 TOL = 1e-5                     # north-star relative waveform tolerance
@@ -692,6 +693,17 @@ def roofline_block(n_fft, units, kern_ms):
             roof["frac_at_held_clock"] = pmc.get("valu_frac")
         if pmc.get("valu_issue_cycles_source"):
             roof["issue_cycles_source"] = pmc["valu_issue_cycles_source"]
+        # the same instruction counts priced at what a dense independent stream
+        # sustains on the part (tools/micro/valu_peak.hip, 8 waves/SIMD, shader
+        # cycles from s_memtime: v_fma_f32 2.71, v_exp_f32 4.86 per wave-
+        # instruction; profiles/r04_micro_valu_peak.txt) at the profiled clock:
+        # how close the kernel runs to a VALU stream with no dependencies, LDS or
+        # barriers at all, rather than to the datasheet's 2 cycles
+        vi, tr = pmc.get("valu_insts_scalar_equiv"), pmc.get("trans_insts")
+        if vi and tr is not None and pmc.get("clock_ghz_profiled"):
+            dense = DENSE_VALU_CYC * (vi - tr) + DENSE_TRANS_CYC * tr
+            roof["dense_stream_cycles"] = dense
+            roof["frac_vs_dense_stream"] = dense / (SIMDS * pmc["clock_ghz_profiled"] * 1e9 * ks)
         for k in ("share_wait_inst_any", "lds_conflict_cycles_per_lds_inst", "vgprs"):
             if pmc.get(k) is not None:
                 roof[k] = pmc[k]

@@ -41,7 +41,6 @@
 // outputs themselves are f32 (the enhance kernel's output type).
 #include "cse_common.hpp"
 
-#include <cstdlib>
 #include <type_traits>
 
 namespace cse {
@@ -72,32 +71,9 @@ constexpr int SROW = 43;                 // staging: 8 rows (sample mod 8) x 43 
 // boundary; 4,096 cells 4.30 / 4.35 -> 4.29 / 4.28 ms)
 constexpr int SSTR = 347;
 static_assert(SSTR >= 8 * SROW && SSTR % 64 == GRP, "staging slot stride");
-// i8-sliced resampler (MF, clipped cells): the FIR as a Hankel GEMM on the
-// matrix pipe.  Row (slot, a), a < 9, holds the 15 outputs 5(q0 + 3a + m) + r
-// (m < 3, r < 5) = sum over k' < 139 of e[8(q0 + 3a) - 58 + k'] c_r[k' - 8m]:
-// A[row][k'] = the slot's staged sample 24a + k', B[k'][5m + r] = c_r[k' - 8m].
-// The clipped sample is fixed point E = rint(e 2^38) in 5 balanced base-256
-// digits (planes of int8), the coefficient C = rint(c 2^47) in 6; the digit
-// pairs i + j <= MF_S (CSE_STOI_MF_S, default 4) accumulate exactly in int32
-// per s = i + j (6 x 139 x 128^2 < 2^31) and out = 2^-53 sum_s acc_s
-// 256^(5 - s).  The dropped pairs i + j > MF_S weigh below 2^(-33 - 8 (MF_S - 4))
-// of full scale (MF_S = 4: 2^-33; measured 7.4e-11 in STOI against the fp64
-// FIR over 4,096 10-s cells).  v_mfma_i32_16x16x64_i8: K in 3 chunks of 64 (139 used), 16
-// columns (15 used); lane l holds k = 16 (l >> 4) + b of its row / column l & 15
-// (any k map shared by A and B is exact: tools/micro/mfma_i8_layout.hip).
-constexpr int MF_ED = 5, MF_CD = 6, MF_KC = 3;
-#ifndef CSE_STOI_MF_S
-#define CSE_STOI_MF_S 4  // digit pairs kept: i + j <= CSE_STOI_MF_S (4: 7e-11 of the fp64 FIR)
-#endif
-constexpr int MF_S = CSE_STOI_MF_S;
-// Bf[j] indexes the MF_CD coefficient digit planes (j <= MF_S) and the scale
-// 256^(5 - MF_S) must be a non-negative shift
-static_assert(MF_S >= 0 && MF_S <= MF_CD - 1, "CSE_STOI_MF_S must lie in [0, 5]");
-constexpr int MF_PL = 384;                  // bytes per digit plane and slot (>= 24 * 8 + 192)
-constexpr int MF_SL = MF_ED * MF_PL;        // bytes per slot
-constexpr int MF_SLOTS = 7;                 // slots per chunk: 63 rows = 4 tiles, one per wave
-constexpr int MF_BTAB = MF_CD * MF_KC * 4 * 16 * 16;  // coefficient digit fragments (bytes)
-constexpr int STAGE_F = (MF_SL * MF_SLOTS / 4 > SLOTS * SSTR) ? MF_SL * MF_SLOTS / 4 : SLOTS * SSTR;
+// (r03's opt-in i8-sliced resampler on the matrix pipe, level with this fp64 FIR
+// at best, left the product in r04: tools/stoi_mf.md says how to rebuild it)
+constexpr int STAGE_F = SLOTS * SSTR;
 constexpr int NT = 256;                  // threads per workgroup
 constexpr double EPS = 2.220446049250313e-16; // np.finfo(float).eps
 __constant__ int BAND_EDGE[NBAND + 1] = {7, 9, 11, 14, 17, 22, 27, 34, 43, 55,
@@ -106,7 +82,7 @@ __constant__ int BAND_EDGE[NBAND + 1] = {7, 9, 11, 14, 17, 22, 27, 34, 43, 55,
 
 struct StoiLayout {
     int64_t n10, F, Mmax, Jmax, NBLK;
-    int64_t coef64, coefq, meta, x10, en, kf, btab, xtob, xstat, total;
+    int64_t coef64, meta, x10, en, kf, btab, xtob, xstat, total;
 };
 
 static inline int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
@@ -121,7 +97,6 @@ static StoiLayout stoi_layout(int64_t n_sig, int64_t len) {
     L.NBLK = (L.Mmax + MINF - 1) / MINF + 1;
     int64_t o = 0;
     L.coef64 = o; o = align256(o + 5 * CST * 8);
-    L.coefq = o;  o = align256(o + MF_BTAB);
     L.meta = o;   o = align256(o + n_sig * META * 4);
     L.x10 = o;    o = align256(o + n_sig * L.n10 * 8);
     L.en = o;     o = align256(o + n_sig * L.F * 8);
@@ -182,29 +157,6 @@ __global__ void __launch_bounds__(1024) stoi_coef_kernel(double* coef64) {
         if (kk < KN && d >= -HALF_LEN && d <= HALF_LEN) v = UP * h[HALF_LEN + d] / total;
         coef64[i] = v;
     }
-}
-
-// prepare 1b: the coefficients as B fragments of the i8 GEMM, digit j of
-// C = rint(c 2^47) (6 balanced base-256 digits, j = 0 most significant), at
-// [j][chunk][k group][column][16 bytes]: lane l reads its 16 bytes in one load
-__global__ void __launch_bounds__(256) stoi_coefq_kernel(const double* __restrict__ coef64,
-                                                          signed char* __restrict__ coefq) {
-    using namespace stoi;
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= MF_BTAB) return;
-    const int b = e & 15, n = (e >> 4) & 15, g = (e >> 8) & 3, jc = e >> 10;
-    const int c = jc % MF_KC, j = jc / MF_KC;
-    const int kp = 64 * c + 16 * g + b;
-    const int m = n / 5, r = n - 5 * m;
-    const int kk = kp - 8 * m;
-    const double v = (n < 15 && kk >= 0 && kk < KN) ? coef64[r * CST + kk] : 0.0;
-    long long x = (long long)rint(v * 0x1p47);
-    int d = 0;
-    for (int t = MF_CD - 1; t >= j; --t) {
-        d = (int)(((x + 128) & 255) - 128);
-        x = (x - d) >> 8;
-    }
-    coefq[e] = (signed char)d;
 }
 
 // prepare 2: clean resampled to 10 kHz in fp64; one thread per phase group
@@ -438,7 +390,7 @@ struct StoiLds {
     cd tw512[256];          // e^{-2πi k/512}
     union {
         struct {
-            // 16-kHz input: f32 as the cells hold it, or (MF) its digit planes
+            // 16-kHz input, f32 as the cells hold it
             float stage[stoi::STAGE_F];
             double e10[stoi::MAXD][stoi::HOP];
         } a;
@@ -477,31 +429,11 @@ __device__ __forceinline__ void stoi_tables(StoiLds& L) {
 
 // PRE: the 10-kHz signal is given (clean side, fp64 x10); otherwise the 16-kHz
 // cell output is resampled here.
-typedef int mf_i4 __attribute__((ext_vector_type(4)));
-
-// E = rint(e 2^38) of a sample in [-1, 1] as 5 balanced base-256 digits (d[0]
-// most significant), through two exact f32 halves: hi = rint(e 2^14), the
-// remainder e - hi 2^-14 is exact, lo = rint(remainder 2^38), E = hi 2^24 + lo
-__device__ __forceinline__ void mf_digits(float e, int (&d)[stoi::MF_ED]) {
-    const float hf = rintf(e * 0x1p14f);
-    int lo = (int)rintf((e - hf * 0x1p-14f) * 0x1p38f);
-    int hi = (int)hf;
-#pragma unroll
-    for (int t = 4; t >= 2; --t) {
-        d[t] = ((lo + 128) & 255) - 128;
-        lo = (lo - d[t]) >> 8;
-    }
-    hi += lo;  // the carry out of the low 24 bits (|lo| <= 1 here)
-    d[1] = ((hi + 128) & 255) - 128;
-    d[0] = (hi - d[1]) >> 8;
-}
-
-template <bool PRE, bool MF = false>
+template <bool PRE>
 __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t len, int lag,
                              bool clip, const double* __restrict__ x10,
                              const double* __restrict__ coef, const int* __restrict__ btab,
-                             int nblk, double* __restrict__ env,
-                             const signed char* __restrict__ coefq = nullptr) {
+                             int nblk, double* __restrict__ env) {
     using namespace stoi;
     const int tid = threadIdx.x;
     // 16-kHz input samples of one staging chunk, loaded into registers one
@@ -513,7 +445,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
     // Lane tid stages slot fs = tid / FW (FW = 28 lanes per slot, 9 slots), samples
     // uu = fr + FW u: one block-table read and one base index per fetch, the
     // loads at constant strides from it
-    constexpr int NSL = MF ? MF_SLOTS : SLOTS;            // slots per chunk
+    constexpr int NSL = SLOTS;                            // slots per chunk
     constexpr int FW = 28, NU = 8 * GRP + KN;             // NU = 339 samples staged per slot
     constexpr int PF = (NU + FW - 1) / FW;                // 13 loads per lane
     static_assert(SLOTS * FW <= NT, "staging lanes");
@@ -560,26 +492,15 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
         } else {
             for (int c0 = 0; c0 < D; c0 += NSL) {
                 const int ns = min(NSL, D - c0);
-                // stage e[8 q0 - 58 + uu], uu < 339, at [uu & 7][uu >> 3] (MF:
-                // its 5 digits at byte uu of the slot's digit planes)
+                // stage e[8 q0 - 58 + uu], uu < 339, at [uu & 7][uu >> 3]
                 if (fs < ns) {
                     float* st = L.u.a.stage + fs * SSTR;
-                    signed char* pl = (signed char*)L.u.a.stage + fs * MF_SL;
 #pragma unroll
                     for (int u = 0; u < PF; ++u) {
                         const int uu = fr + FW * u;
                         float v = (unsigned)(fbase + FW * u) < (unsigned)cnt ? pre[u] : 0.0f;
                         if (clip) v = fminf(fmaxf(v, -1.0f), 1.0f);
-                        if (u < PF - 1 || uu < NU) {
-                            if (MF) {
-                                int dg[MF_ED];
-                                mf_digits(v, dg);
-#pragma unroll
-                                for (int i = 0; i < MF_ED; ++i) pl[i * MF_PL + uu] = (signed char)dg[i];
-                            } else {
-                                st[(uu & 7) * SROW + (uu >> 3)] = v;
-                            }
-                        }
+                        if (u < PF - 1 || uu < NU) st[(uu & 7) * SROW + (uu >> 3)] = v;
                     }
                 }
                 __syncthreads();  // stage (and the next block's table) visible
@@ -587,62 +508,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                     fetch(tb, c0 + NSL);
                 else if (blk + 1 < nblk)
                     fetch(tn, 0);
-                if (MF) {
-                    // GEMM tiles of 16 rows (slot, a) over the chunk's ns * 9 rows,
-                    // one wave per tile (7 slots: 63 rows, 4 tiles)
-                    const int wv = tid >> 6, ln = tid & 63;
-                    const int nrows = ns * 9;
-                    for (int tile = wv; tile * 16 < nrows; tile += NT / 64) {
-                        const int row = tile * 16 + (ln & 15);
-                        const int rw = row < nrows ? row : 0;  // rows past the chunk read slot 0
-                        const signed char* ab = (const signed char*)L.u.a.stage + (rw / 9) * MF_SL +
-                                                24 * (rw % 9) + 16 * (ln >> 4);
-                        mf_i4 acc[MF_S + 1];
-#pragma unroll
-                        for (int t = 0; t <= MF_S; ++t) acc[t] = mf_i4{0, 0, 0, 0};
-#pragma unroll 1
-                        for (int c = 0; c < MF_KC; ++c) {
-                            mf_i4 A[MF_ED], Bf[MF_S + 1];
-#pragma unroll
-                            for (int i = 0; i < MF_ED; ++i) {
-                                const int2* a2 = (const int2*)(ab + i * MF_PL + 64 * c);
-                                const int2 lo2 = a2[0], hi2 = a2[1];
-                                A[i] = mf_i4{lo2.x, lo2.y, hi2.x, hi2.y};
-                            }
-#pragma unroll
-                            for (int j = 0; j <= MF_S; ++j)
-                                Bf[j] = *(const mf_i4*)(coefq + (((j * MF_KC + c) * 4 + (ln >> 4)) * 16 +
-                                                                 (ln & 15)) * 16);
-#pragma unroll
-                            for (int i = 0; i < MF_ED; ++i)
-#pragma unroll
-                                for (int j = 0; j <= MF_S; ++j)
-                                    if (i + j <= MF_S)
-                                        acc[i + j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
-                                            A[i], Bf[j], acc[i + j], 0, 0, 0);
-                        }
-                        // C: column ln & 15 = 5 m + r, rows 4 (ln >> 4) + reg
-                        const int n = ln & 15;
-                        if (n < 15) {
-                            const int m = n / 5, r = n - 5 * m;
-#pragma unroll
-                            for (int reg = 0; reg < 4; ++reg) {
-                                const int crow = tile * 16 + 4 * (ln >> 4) + reg;
-                                if (crow < nrows) {
-                                    const int sl = crow / 9, a = crow - 9 * (crow / 9);
-                                    double h = (double)acc[0][reg];
-#pragma unroll
-                                    for (int t = 1; t <= MF_S; ++t) h = fma(h, 256.0, (double)acc[t][reg]);
-                                    h *= (double)(1ll << (8 * (5 - MF_S)));  // 256^(5 - S)
-                                    const int p = tb[T_P + c0 + sl];
-                                    const int q = (HOP * p) / UP + 3 * a + m;
-                                    const int off = 5 * q + r - HOP * p;
-                                    if (off >= 0 && off < HOP) L.u.a.e10[c0 + sl][off] = h * 0x1p-53;
-                                }
-                            }
-                        }
-                    }
-                } else if (tid < ns * GRP) {
+                if (tid < ns * GRP) {
                     const int s = tid / GRP, g = tid - s * GRP;
                     const int64_t p = tb[T_P + c0 + s];
                     const int64_t q0 = (HOP * p) / UP;
@@ -837,7 +703,6 @@ struct StoiArgs {
     int64_t len, NBLK, Mmax, Jmax;
     int clip;
     const double* coef;
-    const signed char* coefq;  // i8 GEMM coefficient fragments (MF)
     const int* meta;
     const int* btab;
     const double* xtob;
@@ -849,7 +714,6 @@ struct StoiArgs {
 // coef is a separate const __restrict__ argument so the compiler can prove it
 // is never written and read it through the scalar cache (s_load): inside the
 // argument struct it became per-lane vector loads waited on right after issue
-template <bool MF>
 __global__ void __launch_bounds__(stoi::NT, 3) stoi_cells_kernel(StoiArgs a,
                                                               const double* __restrict__ coef) {
     using namespace stoi;
@@ -869,9 +733,8 @@ __global__ void __launch_bounds__(stoi::NT, 3) stoi_cells_kernel(StoiArgs a,
     stoi_tables(L);
     double* env = a.scratch + c * a.Mmax * 16;
     const int lag = a.lag ? a.lag[c] : 0;
-    stoi_phase_a<false, MF>(L, a.y + a.y_offset[c], a.len, lag, a.clip != 0, nullptr, coef,
-                            a.btab + (int64_t)sig * a.NBLK * BT, a.meta[META * sig + 4], env,
-                            a.coefq);
+    stoi_phase_a<false>(L, a.y + a.y_offset[c], a.len, lag, a.clip != 0, nullptr, coef,
+                        a.btab + (int64_t)sig * a.NBLK * BT, a.meta[META * sig + 4], env);
     __syncthreads();  // env rows of this workgroup are visible to it
     // ---- phase B: segment j, band b
     const double* xt = a.xtob + (int64_t)sig * a.Mmax * 16;
@@ -978,8 +841,6 @@ extern "C" int cse_stoi_prepare(const double* clean, int64_t n_sig, int64_t len,
     double* xtob = (double*)(ws + L.xtob);
     double4* xstat = (double4*)(ws + L.xstat);
     hipLaunchKernelGGL(stoi_coef_kernel, dim3(1), dim3(1024), 0, st, coef64);
-    hipLaunchKernelGGL(stoi_coefq_kernel, dim3(ceil_div(stoi::MF_BTAB, 256)), dim3(256), 0, st,
-                       (const double*)coef64, (signed char*)(ws + L.coefq));
     const int64_t groups = (L.n10 + 4) / 5;
     hipLaunchKernelGGL(stoi_resample_clean_kernel, dim3(ceil_div(groups, 256), (unsigned)n_sig),
                        dim3(256), 0, st, clean, len, L.n10, (const double*)coef64, x10);
@@ -1021,23 +882,14 @@ extern "C" int cse_stoi_cells(const float* y, const int64_t* y_offset, const int
     a.Jmax = L.Jmax;
     a.clip = clip;
     a.coef = (const double*)(ws + L.coef64);
-    a.coefq = (const signed char*)(ws + L.coefq);
     a.meta = (const int*)(ws + L.meta);
     a.btab = (const int*)(ws + L.btab);
     a.xtob = (const double*)(ws + L.xtob);
     a.xstat = (const double4*)(ws + L.xstat);
     a.scratch = (double*)scratch;
     a.out = stoi_out;
-    // clipped cells (the sweep's finalize_enhanced output lies in [-1, 1]) may
-    // take the i8-sliced resampler (CSE_STOI_MF=1, experimental); the fp64 FIR
-    // otherwise
-    static const bool want_mf = getenv("CSE_STOI_MF") && getenv("CSE_STOI_MF")[0] == '1';
-    if (clip && want_mf)
-        hipLaunchKernelGGL(stoi_cells_kernel<true>, dim3((unsigned)n_cells), dim3(stoi::NT), 0,
-                           (hipStream_t)stream, a, a.coef);
-    else
-        hipLaunchKernelGGL(stoi_cells_kernel<false>, dim3((unsigned)n_cells), dim3(stoi::NT), 0,
-                           (hipStream_t)stream, a, a.coef);
+    hipLaunchKernelGGL(stoi_cells_kernel, dim3((unsigned)n_cells), dim3(stoi::NT), 0,
+                       (hipStream_t)stream, a, a.coef);
     CSE_CHECK_LAUNCH("cse_stoi_cells");
     return CSE_OK;
 }

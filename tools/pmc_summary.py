@@ -131,6 +131,8 @@ def main(tag, rnd, units512=None, units1024=None):
             k512["valu_frac"] = sd["valu_issue_cycles"] / (SIMDS * busy / 32)
             k512["valu_issue_cycles_source"] = ("scalar build (CSE_PK=0) instruction counts: a packed f32 "
                                                 "instruction does the work of two scalar ones")
+            k512["valu_insts_scalar_equiv"] = spmc.get("SQ_INSTS_VALU")
+            k512["trans_insts"] = spmc.get("SQ_INSTS_VALU_TRANS_F32")
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
     json.dump(summary, open(os.path.join(REPO, "profiles", f"{rnd}_kernels.json"), "w"), indent=1)
     for key, units in (("enhance512", units512), ("enhance1024", units1024)):
@@ -147,6 +149,8 @@ def main(tag, rnd, units512=None, units1024=None):
                "valu_frac": k.get("valu_frac"), "clock_ghz_profiled": k.get("clock_ghz_profiled"),
                "valu_issue_cycles": k.get("valu_issue_cycles"),
                "valu_issue_cycles_source": k.get("valu_issue_cycles_source", "this build's counts"),
+               "valu_insts_scalar_equiv": k.get("valu_insts_scalar_equiv", pmc.get("SQ_INSTS_VALU")),
+               "trans_insts": k.get("trans_insts", pmc.get("SQ_INSTS_VALU_TRANS_F32")),
                "share_wait_inst_any": k.get("share_wait_inst_any"),
                "lds_conflict_cycles_per_lds_inst": k.get("lds_conflict_cycles_per_lds_inst"),
                "kernel_src_sha": src_sha,
