@@ -187,17 +187,17 @@ __device__ __forceinline__ f2 pdup(float s) { return f2{s, s}; }
 // Forms with a negation of one lane, written out: the compiler would take a
 // constant pair such as (-1, 1) from two SGPRs for each (and the kernel ran out
 // of SGPRs); VOP3P's op_sel / neg_lo / neg_hi do it in the instruction.
-#define CSE_PK2(name, mods, expr)                                          \
+#define CSE_PK2(name, mods)                                                \
     __device__ __forceinline__ f2 name(f2 a, f2 b) {                      \
         f2 r;                                                              \
         asm("v_pk_add_f32 %0, %1, %2 " mods : "=v"(r) : "v"(a), "v"(b)); \
         return r;                                                          \
     }
 // a + i b = (a.x - b.y, a.y + b.x);  a - i b = (a.x + b.y, a.y - b.x)
-CSE_PK2(p_addi, "op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]", )
-CSE_PK2(p_subi, "op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]", )
+CSE_PK2(p_addi, "op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]")
+CSE_PK2(p_subi, "op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]")
 // conj(a) + i conj(b) = (a.x + b.y, -a.y + b.x)
-CSE_PK2(p_conj_addi, "op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[1,0]", )
+CSE_PK2(p_conj_addi, "op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[1,0]")
 #undef CSE_PK2
 // (b.x - b.y, b.x + b.y) and (-b.x - b.y, b.x - b.y): r2-scaled rho b of idft4_tw
 __device__ __forceinline__ f2 p_rot1(f2 b) {
@@ -210,7 +210,8 @@ __device__ __forceinline__ f2 p_rot3(f2 b) {
     asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1] neg_lo:[1,1] neg_hi:[0,1]" : "=v"(r) : "v"(b));
     return r;
 }
-// c + i k b = (c.x - k b.y, c.y + k b.x) and c - i k b, k a broadcast pair
+// c + i k b = (c.x - k b.y, c.y + k b.x) and c - i k b, k a broadcast pair of
+// compile-time constants (an SGPR pair: "s" requires a wave-uniform value)
 __device__ __forceinline__ f2 p_fma_i(f2 b, f2 k, f2 c) {
     f2 r;
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[1,0,0]"

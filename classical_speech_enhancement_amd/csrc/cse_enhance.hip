@@ -166,7 +166,7 @@ constexpr float kLsaC = 0.26438318647244886f;  // 0.5 log2(log2 e)
 // gclip = min(gain_floor, 1): the lower bound of the final np.clip
 __device__ __forceinline__ float gain_omlsa(float gam2, float dd, float& rr, float a_rr,
                                             float ksi_min, float gclip, float lg2_floor,
-                                            float lgf_c, float q, float vmax2) {
+                                            float lgf_c, float eq, float cq, float vmax2) {
     const float xi = fmaxf(fmaf(a_rr, rr, dd), ksi_min);
     const float r = fast_rcp(1.0f + xi);
     const float xr = xi * r;
@@ -176,11 +176,13 @@ __device__ __forceinline__ float gain_omlsa(float gam2, float dd, float& rr, flo
     const float dn = horner(CSE_LSAD, vc2);
     const float L = fast_log2(xr * __builtin_amdgcn_rsqf(vc2));
     const float ev = fast_exp2(v2);
-    const float A = q * (r * ev) + 1e-10f;
-    // A >= 1e-10 and 1 - q > 0: p = A/(A + 1 - q) lies in (0, 1) up to a rounding,
-    // so the reference's clip (advanced_mmse.py:116) needs no instruction
+    // A = q Lambda + 1e-10 divided by q: A' = Lambda + eq (eq = 1e-10 / q), and
+    // p = A / (A + 1 - q) = A' / (A' + cq) (cq = (1 - q) / q): one multiply less.
+    // A' > 0 and cq > 0: p lies in (0, 1) up to a rounding, so the reference's
+    // clip (advanced_mmse.py:116) needs no instruction
+    const float A = fmaf(r, ev, eq);
     const float num = fmaf(L - lgf_c, dn, pn);
-    const float den = (A + (1.0f - q)) * dn;
+    const float den = (A + cq) * dn;
     const float g = fast_exp2(fmaf(A * num, fast_rcp(den), lg2_floor));
     const float G = __builtin_amdgcn_fmed3f(g, gclip, 1.0f);  // g >= 0, never NaN
     rr = (G * G) * gam2;
@@ -307,7 +309,9 @@ __device__ __forceinline__ void wave_sync() {
 
 // per-cell parameters as the gain stage wants them
 struct CellParam {
-    float p0, p1, p2, p3, p4, lg2_floor, q_spp, gclip;  // gclip: OMLSA min(gain_floor, 1)
+    // OMLSA: q_spp = 1e-10 / q and p3 = (1 - q) / q (q clamped to [1e-3, 1 - 1e-3]),
+    // gclip = min(gain_floor, 1)
+    float p0, p1, p2, p3, p4, lg2_floor, q_spp, gclip;
 };
 static_assert(sizeof(CellParam) == 32, "CellParam layout");
 
@@ -367,7 +371,7 @@ __device__ __forceinline__ float gain_bin(float2& y, RowV rv, float& rr, float a
         g = gain_mmse(rv.g, dd, cig, rr, alpha_t, cp.p1, cp.p2, cp.p3);
     } else {
         g = gain_omlsa(rv.g, dd, rr, alpha_t * kLn2, cp.p1, cp.gclip, cp.lg2_floor,
-                       cp.lg2_floor - kLsaC, cp.q_spp, cp.p4 * kLog2e);
+                       cp.lg2_floor - kLsaC, cp.q_spp, cp.p3, cp.p4 * kLog2e);
     }
     return g;
 }
@@ -445,9 +449,9 @@ __device__ __forceinline__ f2 gain_pair(f2 gam, f2 d, f2 a, f2& rr, float alpha_
         const f2 xs = xr * f2{__builtin_amdgcn_rsqf(vc2.x), __builtin_amdgcn_rsqf(vc2.y)};
         const f2 L = f2{fast_log2(xs.x), fast_log2(xs.y)};
         const f2 ev = f2{fast_exp2(v2.x), fast_exp2(v2.y)};
-        const f2 A = pfma(pdup(cp.q_spp), r * ev, pdup(1e-10f));
+        const f2 A = pfma(r, ev, pdup(cp.q_spp));  // A / q, see gain_omlsa
         const f2 num = pfma(L - pdup(cp.lg2_floor - kLsaC), dn, pn);
-        const f2 den = (A + pdup(1.0f - cp.q_spp)) * dn;
+        const f2 den = (A + pdup(cp.p3)) * dn;
         const f2 e = pfma(A * num, prcp(den), pdup(cp.lg2_floor));
         const f2 G = pmed3(f2{fast_exp2(e.x), fast_exp2(e.y)}, cp.gclip, 1.0f);
         rr = (G * G) * gam;
@@ -765,7 +769,12 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         prm.p3 = cp->param[3];
         prm.p4 = cp->param[4];
         prm.lg2_floor = (ALGO == CSE_ALGO_OMLSA) ? fast_log2(prm.p2) : 0.0f;
-        prm.q_spp = fminf(fmaxf(prm.p3, 1e-3f), 1.0f - 1e-3f);
+        prm.q_spp = 0.0f;
+        if (ALGO == CSE_ALGO_OMLSA) {  // see gain_omlsa: A and p divided by q
+            const double q = fmin(fmax((double)prm.p3, 1e-3), 1.0 - 1e-3);
+            prm.q_spp = (float)(1e-10 / q);
+            prm.p3 = (float)((1.0 - q) / q);
+        }
         prm.gclip = 0.0f;
         // clip bounds for one v_med3: the lower bound capped at the upper one
         // (numpy's clip returns the upper bound when they cross)

@@ -113,3 +113,31 @@ def test_job_units_match_shards():
         _, local, _, units, _ = bench.rank_job(_Args, 8, rank, 512)
         total += len(local)
     assert total == len(specs) and units == 100 * 4572372
+
+
+@pytest.mark.parametrize("n_fft", [512, 1024])
+def test_roofline_block_prices_the_committed_pmc(n_fft):
+    """The line's VALU roofline from the committed PMC of this build
+    (profiles/pmc_enhance{n_fft}_r04.json, digest-matched): frac = the issue
+    cycles (VALU 2, transcendental 4 per wave64 instruction) / (1024 SIMDs x
+    2.4 GHz x kernel time), and frac_vs_dense_stream = the same instruction
+    counts at the rates tools/micro/valu_peak.hip measured (2.71 / 4.86
+    cycles) over the profiled clock.  No bandwidth is derived from SURVEY
+    8(d)'s nominal bytes."""
+    import json
+    units = 457237200
+    pmc = bench.load_pmc(units, n_fft)
+    if not pmc or pmc.get("kernel_src_sha") != bench.kernel_src_sha():
+        pytest.skip("no committed PMC profile of these kernel sources")
+    ks_ms = pmc["kernel_ms"]
+    r = bench.roofline_block(n_fft, units, ks_ms)
+    assert r["bound"] == "valu" and r["pmc_matches_build"]
+    ks = ks_ms / 1e3
+    assert abs(r["frac"] - pmc["valu_issue_cycles"] / (bench.SIMDS * bench.CLOCK * ks)) < 1e-12
+    v, t = pmc["valu_insts_scalar_equiv"], pmc["trans_insts"]
+    dense = bench.DENSE_VALU_CYC * (v - t) + bench.DENSE_TRANS_CYC * t
+    assert abs(r["frac_vs_dense_stream"] - dense / (bench.SIMDS * pmc["clock_ghz_profiled"] * 1e9 * ks)) < 1e-12
+    # the committed profile: the datasheet fraction below 1, the dense-stream one near it
+    assert 0.5 < r["frac"] < 1.0 and 0.8 < r["frac_vs_dense_stream"] < 1.1
+    assert all("GBps" not in k or (r[k] or 0) < 8000 for k in r)
+    json.dumps(r)  # the line must serialise
