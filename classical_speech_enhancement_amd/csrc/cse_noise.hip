@@ -527,6 +527,10 @@ struct Workspace {
 
 static int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
+// threads of a whole-row workgroup for the per-bin recurrences (iir, finish):
+// the bins of one frame row in one workgroup, whole wavefronts, <= 1,024
+static int row_threads(int B) { return B >= 1024 ? 1024 : ((B + 63) / 64) * 64; }
+
 static Workspace carve(void* ws, int64_t n_sig, int T, int B) {
     unsigned char* p = (unsigned char*)ws;
     Workspace w;
@@ -632,7 +636,8 @@ static int launch_min_tracking(const double* P, const double* med, int64_t n_sig
     int win = prm.window_size > 3 ? prm.window_size : 3;  // min(max(3, w), T), made odd (:97-99)
     if (win > T) win = T;
     if (win % 2 == 0) win += 1;
-    hipLaunchKernelGGL(iir_kernel, dim3(ceil_div(B, 64), (unsigned)n_sig), dim3(64), 0, s, P, T, B,
+    hipLaunchKernelGGL(iir_kernel, dim3(ceil_div(B, row_threads(B)), (unsigned)n_sig),
+                       dim3(row_threads(B)), 0, s, P, T, B,
                        a, w.S);
     if (win / 2 <= MF_HMAX) {
         hipLaunchKernelGGL(min_filter_tiled_kernel,
@@ -792,8 +797,12 @@ extern "C" int cse_noise_finish(const cse_noise_job_t* jobs, int n_jobs, int64_t
                   "cse_noise_finish: bad arguments");
     CSE_CHECK_ARG(n_sig > 0 && n_sig < 65536 && B >= 1, "cse_noise_finish: bad shape");
     if (n_jobs == 0) return CSE_OK;
-    hipLaunchKernelGGL(finish_kernel, dim3(ceil_div(B, 64), (unsigned)n_sig, (unsigned)n_jobs),
-                       dim3(64), 0, (hipStream_t)stream, jobs, B, src, dst);
+    // one workgroup per (signal, job) row, up to 1,024 threads: the row's frame
+    // writes leave one workgroup (one XCD's L2) as whole lines, where 64-bin
+    // workgroups spread a 1,028-B row over up to five XCDs
+    const int nt = row_threads(B);
+    hipLaunchKernelGGL(finish_kernel, dim3(ceil_div(B, nt), (unsigned)n_sig, (unsigned)n_jobs),
+                       dim3(nt), 0, (hipStream_t)stream, jobs, B, src, dst);
     CSE_CHECK_LAUNCH("cse_noise_finish");
     return CSE_OK;
 }

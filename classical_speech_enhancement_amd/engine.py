@@ -305,7 +305,10 @@ class GridPlan:
                 k = key_cache[ck] = (hop, noise_key(alg, p, n_frames(L, hop)))
                 keys.setdefault(k, None)
             item_key.append(k)
-        self.keys = list(keys)
+        # jobs grouped by hop: each hop's rows are finished right after its own
+        # estimates (one cse_noise_finish launch per hop), so the first hop's
+        # finish can run while the next hop's chain does
+        self.keys = sorted(keys, key=lambda k: k[0])
         self.pool_off, noff = {}, 0
         self.raw_off, roff = {}, 0
         jobs = []
@@ -336,6 +339,10 @@ class GridPlan:
             jt[j] = (so, do, sf, of, mu, ie)
         self.n_jobs = len(jobs)
         self.jobs_d = torch.from_numpy(jt.view(np.uint8).copy()).to(dev)
+        self.hop_jobs = {}  # hop -> (first job, count)
+        for j, (hop, _) in enumerate(self.keys):
+            first, cnt = self.hop_jobs.get(hop, (j, 0))
+            self.hop_jobs[hop] = (first, cnt + 1)
         self.med = torch.empty((S, B), dtype=torch.float64, device=dev)
         Tmax = max(n_frames(L, h) for h in self.hops)
         self.ws = torch.empty(int(eng.lib.cse_noise_workspace_bytes(S, Tmax, B)),
@@ -465,8 +472,10 @@ class GridPlan:
                                                          ctypes.byref(prm), float(eps),
                                                          _ptr(raw(b)), None, st),
                                "cse_noise_estimate(true)")
-        _lib.check(lib.cse_noise_finish(_ptr(self.jobs_d), self.n_jobs, S, B, _ptr(self.raw),
-                                        _ptr(self.pool), st), "cse_noise_finish")
+            j0, nj = self.hop_jobs[hop]
+            jobs = ctypes.c_void_p(self.jobs_d.data_ptr() + j0 * _lib.NOISE_JOB_DTYPE.itemsize)
+            _lib.check(lib.cse_noise_finish(jobs, nj, S, B, _ptr(self.raw), _ptr(self.pool), st),
+                       "cse_noise_finish")
         self.clean = clean if self.with_clean else None
 
     def enhance(self):
