@@ -54,11 +54,22 @@ static int next_pow2(int n) {
     return p;
 }
 
-// np.percentile(sorted[0:n], pct) with method='linear' (numpy 2.x _quantile/_lerp)
-__device__ double lerp_percentile(const double* s, int n, double q) {
+// numpy 2.x _lerp(a, b, t): a + (b - a) t, or b - (b - a)(1 - t) for t >= 0.5,
+// every operation rounded on its own (-ffp-contract=fast would fuse the product
+// into the sum: one rounding less than numpy)
+__device__ __forceinline__ double np_lerp(double a, double b, double t) {
+#pragma clang fp contract(off)
+    const double diff = b - a;
+    return t >= 0.5 ? b - diff * (1.0 - t) : a + diff * t;
+}
+
+// numpy 2.x _quantile's indices for method='linear' on n sorted values:
+// virtual index (n - 1) q, its neighbours, and the weight gamma = virtual -
+// previous (rounded operations, as np_lerp)
+__device__ __forceinline__ double np_quantile_index(int n, double q, int& prev, int& next) {
+#pragma clang fp contract(off)
     const double virt = (double)(n - 1) * q;
     double prev_f = floor(virt);
-    int prev, next;
     if (virt >= (double)(n - 1)) {
         prev = next = n - 1;
         prev_f = -1.0;  // numpy sets previous_indexes = -1 here; gamma uses it
@@ -69,11 +80,14 @@ __device__ double lerp_percentile(const double* s, int n, double q) {
         prev = (int)prev_f;
         next = prev + 1;
     }
-    const double gamma = virt - prev_f;
-    const double a = s[prev], b = s[next];
-    const double diff = b - a;
-    if (gamma >= 0.5) return b - diff * (1.0 - gamma);
-    return a + diff * gamma;
+    return virt - prev_f;
+}
+
+// np.percentile(sorted[0:n], pct) with method='linear' (numpy 2.x _quantile/_lerp)
+__device__ double lerp_percentile(const double* s, int n, double q) {
+    int prev, next;
+    const double gamma = np_quantile_index(n, q, prev, next);
+    return np_lerp(s[prev], s[next], gamma);
 }
 
 // mean_b log(max(P[t][b], eps)) per frame: one wavefront per frame (4 per
@@ -236,23 +250,9 @@ __global__ void __launch_bounds__(256) bin_stats_wave_kernel(
         return;
     }
     // np.percentile(..., q, method='linear') as lerp_percentile
-    const double virt = (double)(n - 1) * q;
-    double prev_f = floor(virt);
     int prev, next;
-    if (virt >= (double)(n - 1)) {
-        prev = next = n - 1;
-        prev_f = -1.0;
-    } else if (virt < 0.0) {
-        prev = next = 0;
-        prev_f = 0.0;
-    } else {
-        prev = (int)prev_f;
-        next = prev + 1;
-    }
-    const double gamma = virt - prev_f;
-    const double a = wave_at<E>(v, lane, prev), c = wave_at<E>(v, lane, next);
-    const double diff = c - a;
-    const double pc = (gamma >= 0.5) ? c - diff * (1.0 - gamma) : a + diff * gamma;
+    const double gamma = np_quantile_index(n, q, prev, next);
+    const double pc = np_lerp(wave_at<E>(v, lane, prev), wave_at<E>(v, lane, next), gamma);
     const double est = fmax(pc, floor_rel * med[sig * B + b]);
     if (lane == 0) N[sig * B + b] = (float)fmax(est, eps);
 }
@@ -329,7 +329,18 @@ __global__ void bin_stats_kernel(const double* __restrict__ P, int T, int B, int
     }
 }
 
-// S_t = a*S_{t-1} + (1-a)*P_t (noise_estimation.py:78-82), numpy evaluation order
+// One smoothing step s = a s + (1 - a) x as numpy evaluates it: two rounded
+// products and a rounded sum.  HIP's __dmul_rn / __dadd_rn are plain x * y /
+// x + y, which -ffp-contract=fast fuses into an FMA (one rounding less: the
+// compiled recurrences were not numpy's until late r04); the pragma takes the
+// contract flag off these operations.
+__device__ __forceinline__ double smooth_step(double a, double s, double c, double x) {
+#pragma clang fp contract(off)
+    return a * s + c * x;
+}
+
+// S_t = a*S_{t-1} + (1-a)*P_t (noise_estimation.py:78-82), numpy evaluation order;
+// the loads one block of U frames ahead of the recurrence (finish_row's form)
 __global__ void iir_kernel(const double* __restrict__ P, int T, int B, double a,
                            double* __restrict__ S) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -340,19 +351,32 @@ __global__ void iir_kernel(const double* __restrict__ P, int T, int B, double a,
     double s = Ps[0];
     Ss[0] = s;
     const double c = 1.0 - a;
+    constexpr int U = 8;
+    const int full = 1 + ((T > 1 ? T - 1 : 0) / U) * U;  // frames [1, full) in whole blocks
     int t = 1;
-    for (; t + 8 <= T; t += 8) {  // loads first: the recurrence is the only dependency
-        double x[8];
+    if (full > 1) {
+        double cur[U], nxt[U];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = Ps[(int64_t)(t + u) * B];
+        for (int u = 0; u < U; ++u) cur[u] = Ps[(int64_t)(1 + u) * B];
+        for (; t < full; t += U) {
+            const bool more = t + U < full;  // uniform
+            if (more) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            s = __dadd_rn(__dmul_rn(a, s), __dmul_rn(c, x[u]));
-            Ss[(int64_t)(t + u) * B] = s;
+                for (int u = 0; u < U; ++u) nxt[u] = Ps[(int64_t)(t + U + u) * B];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                s = smooth_step(a, s, c, cur[u]);
+                Ss[(int64_t)(t + u) * B] = s;
+            }
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+            }
         }
     }
     for (; t < T; ++t) {
-        s = __dadd_rn(__dmul_rn(a, s), __dmul_rn(c, Ps[(int64_t)t * B]));
+        s = smooth_step(a, s, c, Ps[(int64_t)t * B]);
         Ss[(int64_t)t * B] = s;
     }
 }
@@ -460,7 +484,7 @@ __global__ void smooth_kernel(const float* __restrict__ N, int T, int B, int src
     const double c = 1.0 - mu;
     for (int t = 1; t < T; ++t) {
         const double n = t < src_frames ? (double)Ns[(int64_t)t * B] : 0.0;  // fix_length pad
-        s = __dadd_rn(__dmul_rn(mu, s), __dmul_rn(c, n));
+        s = smooth_step(mu, s, c, n);
         Os[(int64_t)t * B] = (float)s;
     }
 }
@@ -472,7 +496,58 @@ __global__ void invert_kernel(const float* __restrict__ N, int64_t n, double eps
 }
 
 // batched post-processing of noise rows: smoothing over frames, zero-padding a
-// static row to out_frames (librosa fix_length), optional 1/max(., eps)
+// static row to out_frames (librosa fix_length), optional 1/max(., eps).
+// Frames t < min(src_frames, out_frames) read the source, later ones take 0
+// (the zero pad): s = mu s + (1 - mu) n in fp64 in numpy's order.  The
+// inversion is a template branch and the loads come in whole blocks of U
+// frames, one block ahead, with no per-frame conditions: r03's form (a bounds
+// check per load and per store) compiled to a branch per access and a full
+// vmcnt(0) wait per block.
+template <bool INV>
+__device__ __forceinline__ void finish_row(const float* __restrict__ Ns, float* __restrict__ Os,
+                                           int B, int nsrc, int nfr, double mu, float ief) {
+    const double c = 1.0 - mu;
+    // 1/max(v, eps) in fp32 (correctly rounded 1/x of the rounded operand:
+    // within 1.5 ulp of the fp64 quotient, which the f32 row stores anyway);
+    // the fp64 divide made this launch latency-bound
+    auto out = [&](double v) { return INV ? 1.0f / fmaxf((float)v, ief) : (float)v; };
+    double s = (double)Ns[0];
+    Os[0] = out(s);
+    const int m = nsrc < nfr ? nsrc : nfr;  // frames with a source row
+    constexpr int U = 16;
+    const int full = 1 + ((m > 1 ? m - 1 : 0) / U) * U;  // frames [1, full) in whole blocks
+    int t = 1;
+    if (full > 1) {
+        float cur[U], nxt[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = Ns[(int64_t)(1 + u) * B];
+        for (; t < full; t += U) {
+            const bool more = t + U < full;  // uniform
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) nxt[u] = Ns[(int64_t)(t + U + u) * B];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                s = smooth_step(mu, s, c, (double)cur[u]);
+                Os[(int64_t)(t + u) * B] = out(s);
+            }
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+            }
+        }
+    }
+    for (; t < m; ++t) {
+        s = smooth_step(mu, s, c, (double)Ns[(int64_t)t * B]);
+        Os[(int64_t)t * B] = out(s);
+    }
+    for (; t < nfr; ++t) {  // the zero pad: c * 0 = +0, so s = mu s as in the general form
+        s = smooth_step(mu, s, c, 0.0);
+        Os[(int64_t)t * B] = out(s);
+    }
+}
+
 __global__ void finish_kernel(const cse_noise_job_t* __restrict__ jobs, int B,
                               const float* __restrict__ src, float* __restrict__ dst) {
     const cse_noise_job_t jb = jobs[blockIdx.z];
@@ -481,41 +556,10 @@ __global__ void finish_kernel(const cse_noise_job_t* __restrict__ jobs, int B,
     if (b >= B) return;
     const float* Ns = src + jb.src_offset + sig * (int64_t)jb.src_frames * B + b;
     float* Os = dst + jb.dst_offset + sig * (int64_t)jb.out_frames * B + b;
-    const double mu = jb.mu, c = 1.0 - mu, ie = jb.inv_eps;
-    // 1/max(v, eps) in fp32 (correctly rounded 1/x of the rounded operand:
-    // within 1.5 ulp of the fp64 quotient, which the f32 row stores anyway);
-    // the fp64 divide made this launch latency-bound
-    const float ief = (float)ie;
-    auto put = [&](int t, double v) {
-        Os[(int64_t)t * B] = ie > 0.0 ? 1.0f / fmaxf((float)v, ief) : (float)v;
-    };
-    double s = (double)Ns[0];
-    put(0, s);
-    // software-pipelined: the loads of block k+1 are in flight while block k's
-    // serial recurrence runs (a dependent chain per (signal, bin))
-    constexpr int U = 16;
-    const int nfr = jb.out_frames, nsrc = jb.src_frames;
-    auto fetch = [&](int t0, float (&xs)[U]) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int tt = t0 + u;
-            xs[u] = (tt < nsrc && tt < nfr) ? Ns[(int64_t)tt * B] : 0.0f;
-        }
-    };
-    float cur[U], nxt[U];
-    fetch(1, cur);
-    for (int t = 1; t < nfr; t += U) {
-        fetch(t + U, nxt);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (t + u < nfr) {
-                s = __dadd_rn(__dmul_rn(mu, s), __dmul_rn(c, (double)cur[u]));
-                put(t + u, s);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-    }
+    if (jb.inv_eps > 0.0)
+        finish_row<true>(Ns, Os, B, jb.src_frames, jb.out_frames, jb.mu, (float)jb.inv_eps);
+    else
+        finish_row<false>(Ns, Os, B, jb.src_frames, jb.out_frames, jb.mu, 0.0f);
 }
 
 struct Workspace {

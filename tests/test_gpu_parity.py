@@ -516,3 +516,62 @@ def test_percentile_pairs_equal_single_estimates(P, T_sec):
             for pct in (10.0, 20.0):
                 ref = oracle.percentile_noise(Pc, eps=eps, percentile=pct)
                 assert rel_l2(one[pct][s], np.ravel(ref)) < 1e-6, (T_sec, eps, s, pct)
+
+
+@pytest.mark.parametrize("B", [257, 513])
+def test_noise_finish_jobs_bit_exact(P, B):
+    """cse_noise_finish (the batched noise-row post-processing the engine runs
+    after the estimators) against its numpy restatement, bit for bit: the
+    smoothing s_t = mu s_{t-1} + (1 - mu) n_t in fp64 in numpy's order
+    (mmse.py:48-54, advanced_mmse.py:60-66), the fix_length zero pad of a static
+    row (spectral_subtractor.py:40-41, advanced_mmse.py:54-55: n_t = 0 for t >= 1)
+    and the in-loop floor 1/max(N, eps) in fp32 (wiener_filter.py:58, mmse.py:71,
+    advanced_mmse.py:87).  Frame counts around the kernel's 16-frame load blocks
+    (1, 2, 16, 17, 33, 1,251)."""
+    import torch
+    from classical_speech_enhancement_amd import _lib
+    from classical_speech_enhancement_amd.engine import Engine, _ptr, _stream
+    eng = Engine()
+    lib = eng.lib
+    rng = np.random.default_rng(7)
+    S = 3
+    # (src_frames, out_frames, mu, inv_eps)
+    cases = []
+    for T in (1, 2, 16, 17, 33, 1251):
+        cases += [(T, T, 0.98, 1e-10), (T, T, 0.0, 0.0), (T, T, 0.92, 0.0),
+                  (1, T, 0.95, 1e-10), (1, T, 0.0, 0.0)]
+    cases += [(1, 1, 0.0, 1e-12), (1, 1, 0.5, 0.0)]
+    srcs, src_off, o = [], [], 0
+    for (sf, _, _, _) in cases:
+        a = rng.lognormal(-12.0, 3.0, size=(S, sf, B)).astype(np.float32)
+        a[:, :, ::37] = 0.0  # below any eps: the floor decides
+        srcs.append(a)
+        src_off.append(o)
+        o += a.size
+    src = np.concatenate([a.ravel() for a in srcs])
+    jt = np.zeros(len(cases), dtype=_lib.NOISE_JOB_DTYPE)
+    dst_off, d = [], 0
+    for j, (sf, of, mu, ie) in enumerate(cases):
+        dst_off.append(d)
+        jt[j] = (src_off[j], d, sf, of, mu, ie)
+        d += S * of * B
+    src_d = torch.as_tensor(src).cuda()
+    dst_d = torch.full((d,), np.nan, dtype=torch.float32, device="cuda")
+    jobs_d = torch.from_numpy(jt.view(np.uint8).copy()).cuda()
+    _lib.check(lib.cse_noise_finish(_ptr(jobs_d), len(cases), S, B, _ptr(src_d), _ptr(dst_d),
+                                    _stream()), "cse_noise_finish")
+    out = dst_d.cpu().numpy()
+    for j, (sf, of, mu, ie) in enumerate(cases):
+        n = np.zeros((S, of, B))
+        n[:, :min(sf, of)] = srcs[j][:, :min(sf, of)].astype(np.float64)
+        ref = np.empty((S, of, B))
+        s = n[:, 0].copy()
+        ref[:, 0] = s
+        for t in range(1, of):
+            s = mu * s + (1.0 - mu) * n[:, t]
+            ref[:, t] = s
+        r32 = ref.astype(np.float32)
+        if ie > 0.0:
+            r32 = np.float32(1.0) / np.maximum(r32, np.float32(ie))
+        got = out[dst_off[j]:dst_off[j] + S * of * B].reshape(S, of, B)
+        assert np.array_equal(got, r32), (cases[j], np.abs(got - r32).max())
