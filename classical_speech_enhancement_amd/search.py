@@ -120,6 +120,18 @@ class JobSpecs(list):
         """Global index of the cell computed in place of each of ``ids`` (the
         first identical cell of the same pair and algorithm)."""
         ids = np.asarray(ids, dtype=np.int64)
+        lens = np.asarray(lengths, dtype=np.int64)
+        present = np.zeros(len(lens), dtype=bool)
+        present[self.pair[ids]] = True
+        uL = np.unique(lens[present])
+        if len(uL) <= 1:  # one clip length (the sweep's case): one table lookup per cell
+            if len(uL) == 0:
+                return ids.copy()
+            L = int(uL[0])
+            delta = np.concatenate([self.grid_rep(a, L) - np.arange(len(self.cells[alg]))
+                                    for a, alg in enumerate(self.algorithms)])
+            off = np.concatenate([[0], np.cumsum([len(self.cells[a]) for a in self.algorithms])[:-1]])
+            return ids + delta[off[self.alg[ids]] + self.cell[ids]]
         out = ids.copy()
         for a in range(len(self.algorithms)):
             for L in {int(lengths[q]) for q in np.unique(self.pair[ids[self.alg[ids] == a]])}:
@@ -188,6 +200,10 @@ def cell_costs(specs, lengths):
         hp = np.concatenate([[int(p["hop_length"]) for p in specs.cells[a]] for a in specs.algorithms])
         wt = np.concatenate([[ALGO_WEIGHT.get(a, 1.0)] * len(specs.cells[a])
                              for a in specs.algorithms])
+        n_pairs = len(specs) // max(specs.per_pair, 1)
+        if n_pairs and len(lengths) >= n_pairs and (lengths[:n_pairs] == lengths[0]).all():
+            # one clip length: every pair's block of cells costs the same
+            return np.tile((1 + int(lengths[0]) // hp) * (nf // 2 + 1) * wt, n_pairs)
         off = np.concatenate([[0], np.cumsum([len(specs.cells[a]) for a in specs.algorithms])[:-1]])
         g = off[specs.alg] + specs.cell
         return (1 + lengths[specs.pair] // hp[g]) * (nf[g] // 2 + 1) * wt[g]
@@ -217,6 +233,18 @@ def assign_shards(specs, lengths, world):
         rank_of = np.minimum((mid * world / total).astype(np.int64), world - 1)
     load = np.bincount(rank_of, weights=cost, minlength=world).tolist() if n else [0.0] * world
     return rank_of, load
+
+
+def _unique_inverse(x):
+    """np.unique(x, return_inverse=True) for non-negative integer ids, in O(n)
+    with a mark array instead of a sort (the sweep's 974,400 representatives)."""
+    x = np.asarray(x, dtype=np.int64)
+    if len(x) == 0:
+        return x.copy(), np.zeros(0, dtype=np.int64)
+    mark = np.zeros(int(x.max()) + 1, dtype=bool)
+    mark[x] = True
+    rank = np.cumsum(mark) - 1
+    return np.flatnonzero(mark), rank[x]
 
 
 def engine_compute(clean, noisy, specs, ids, engine=None, align=True, stoi=True):
@@ -262,7 +290,7 @@ def _engine_compute(eng, clean, noisy, specs, ids, align, stoi):
     lengths = [len(x) for x in noisy]
     js_specs = isinstance(specs, JobSpecs)
     if js_specs:
-        comp, back = np.unique(specs.representative(ids, lengths), return_inverse=True)
+        comp, back = _unique_inverse(specs.representative(ids, lengths))
         pair_of = specs.pair[comp]
     else:
         comp, back = ids, np.arange(len(ids))
@@ -288,8 +316,14 @@ def _engine_compute(eng, clean, noisy, specs, ids, align, stoi):
         ev_.synchronize()
         vals[rows_, 3] = np.where(fin_, out_.cpu().numpy(), np.nan)
 
+    sorted_pairs = len(pair_of) < 2 or bool((pair_of[1:] >= pair_of[:-1]).all())
     for L, pairs_l in by_len.items():
-        rows = {p: np.flatnonzero(pair_of == p) for p in pairs_l}
+        if sorted_pairs:  # JobSpecs ids: each pair's cells are one run of comp
+            pa = np.asarray(pairs_l, dtype=np.int64)
+            lo, hi = np.searchsorted(pair_of, pa, "left"), np.searchsorted(pair_of, pa, "right")
+            rows = {p: np.arange(a, b) for p, a, b in zip(pairs_l, lo.tolist(), hi.tolist())}
+        else:
+            rows = {p: np.flatnonzero(pair_of == p) for p in pairs_l}
         batches, cur, n_cur = [], [], 0
         for pair in pairs_l:
             n = len(rows[pair])
@@ -396,14 +430,61 @@ def gather_records(local, n_total, group=None, device=None):
         dist.all_gather_into_tensor(allrec, pad, group=group)
         rec = allrec.cpu()
     rec = rec.numpy()
-    rec = rec[rec[:, 0] >= 0]
-    table = np.full((n_total, NCOL), np.nan)
+    if len(rec) and rec[:, 0].min() < 0:  # padding rows of the shorter shards
+        rec = rec[rec[:, 0] >= 0]
     ids = rec[:, 0].astype(np.int64)
-    if len(np.unique(ids)) != len(ids) or len(ids) != n_total:
+    # every cell exactly once (a count per id: O(n), no sort)
+    inrange = len(ids) == 0 or (ids.min() >= 0 and ids.max() < n_total)
+    seen = np.bincount(ids, minlength=n_total) if inrange and len(ids) else np.zeros(n_total, np.int64)
+    if not inrange or len(ids) != n_total or (len(ids) and seen.max() != 1):
         raise RuntimeError(f"gather: {len(ids)} records for {n_total} cells "
-                           f"({len(ids) - len(np.unique(ids))} duplicates)")
+                           f"({len(ids) - int(np.count_nonzero(seen))} duplicates or out of range)")
+    if np.array_equal(ids, np.arange(n_total)):
+        return rec[:, 1:]  # already in cell order (a view: no copy of the table)
+    table = np.full((n_total, NCOL), np.nan)
     table[ids] = rec[:, 1:]
     return table
+
+
+def _scan_records(sc, rec, ids, tol):
+    """The sequential scan over the strict running maxima of one group (see
+    select_best): returns (winner id or -1, score or None)."""
+    incumbent, win = -1.0, -1
+    for k in rec.tolist():
+        if sc[k] > incumbent + tol:
+            incumbent, win = float(sc[k]), int(ids[k])
+    return win, (incumbent if win >= 0 else None)
+
+
+def _select_best_blocks(specs, table, col, tol):
+    """select_best over a JobSpecs table: each algorithm's cells of all pairs
+    as one [pairs, grid] block (the columns of a (pair, algorithm) run are
+    contiguous), running maxima along the grid axis in one call."""
+    n_pairs = len(specs) // max(specs.per_pair, 1)
+    # the score column with skipped cells at -inf (a finite cell whose score
+    # is not NaN), as [pairs, cells of one pair]
+    sc_all = np.asarray(table[:n_pairs * specs.per_pair, col], dtype=np.float64)
+    ok = (table[:n_pairs * specs.per_pair, 2] != 0) & (sc_all == sc_all)
+    sc_all = np.where(ok, sc_all, -np.inf).reshape(n_pairs, specs.per_pair)
+    found = {}
+    off = 0
+    for a in specs.algorithms:
+        n = len(specs.cells[a])
+        if n:
+            sc = sc_all[:, off:off + n]
+            prev = np.empty_like(sc)
+            prev[:, 0] = -np.inf
+            np.maximum.accumulate(sc[:, :-1], axis=1, out=prev[:, 1:])
+            recs = sc > prev
+            for pair in range(n_pairs):
+                ids = pair * specs.per_pair + off + np.arange(n)
+                found[(pair, a)] = _scan_records(sc[pair], np.flatnonzero(recs[pair]), ids, tol)
+        else:
+            for pair in range(n_pairs):
+                found[(pair, a)] = (-1, None)
+        off += n
+    return OrderedDict(((pair, a), found[(pair, a)]) for pair in range(n_pairs)
+                       for a in specs.algorithms)
 
 
 def select_best(specs, table, objective="snr", tol=None):
@@ -417,6 +498,8 @@ def select_best(specs, table, objective="snr", tol=None):
     if objective not in ("snr", "stoi"):
         raise ValueError(f"objective {objective!r} is not scored on the device (pesq is absent)")
     col = TABLE_COLUMN[objective]
+    if isinstance(specs, JobSpecs) and tol >= 0.0:
+        return _select_best_blocks(specs, table, col, tol)
     groups = OrderedDict()
     if isinstance(specs, JobSpecs):  # (pair, algorithm) runs are contiguous
         per = [len(specs.cells[a]) for a in specs.algorithms]
@@ -434,15 +517,24 @@ def select_best(specs, table, objective="snr", tol=None):
         sc = table[ids, col]
         ok = (table[ids, 2] != 0) & (sc == sc)  # finite cell, score not NaN
         sc = np.where(ok, sc, -np.inf)
-        # the scan's incumbent only ever increases: jump to the first cell
-        # after the current winner that beats it by more than tol
-        incumbent, win, start = -1.0, -1, 0
-        while start < len(ids):
-            hit = np.flatnonzero(sc[start:] > incumbent + tol)
-            if len(hit) == 0:
-                break
-            k = start + int(hit[0])
-            incumbent, win, start = float(sc[k]), int(ids[k]), k + 1
+        incumbent, win = -1.0, -1
+        if tol >= 0.0 and len(sc):
+            # Only a strict running maximum can replace the incumbent: after
+            # any cell j the incumbent is >= sc[j] - tol (it took sc[j], or
+            # sc[j] <= incumbent + tol), so a cell at or below an earlier score
+            # never clears incumbent + tol and leaves the state alone.  The
+            # scan runs over those records only (a few per group).
+            prev = np.maximum.accumulate(np.concatenate(([-np.inf], sc[:-1])))
+            best[key] = _scan_records(sc, np.flatnonzero(sc > prev), ids, tol)
+            continue
+        else:
+            start = 0  # negative tolerance: the plain jump scan
+            while start < len(ids):
+                hit = np.flatnonzero(sc[start:] > incumbent + tol)
+                if len(hit) == 0:
+                    break
+                k = start + int(hit[0])
+                incumbent, win, start = float(sc[k]), int(ids[k]), k + 1
         best[key] = (win, incumbent if win >= 0 else None)
     return best
 

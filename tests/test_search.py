@@ -204,3 +204,61 @@ def test_select_best_columns_equal_the_generic_scan():
     table[:, 3] = rng.random(len(specs))
     for obj in ("snr", "stoi"):
         assert search.select_best(specs, table, obj) == search.select_best(list(specs), table, obj)
+
+
+# ---------------------------------------------------------------------------
+# the sweep's host bookkeeping fast paths (late r04) against their plain forms
+# ---------------------------------------------------------------------------
+def test_unique_inverse_equals_numpy():
+    rng = np.random.default_rng(11)
+    for x in (rng.integers(0, 5000, 20000), np.arange(7), np.zeros(0, np.int64), np.array([3, 3, 3])):
+        c, b = search._unique_inverse(x)
+        uc, ub = np.unique(x, return_inverse=True)
+        assert np.array_equal(c, uc) and np.array_equal(b, ub.ravel())
+
+
+def test_representative_one_length_equals_the_per_length_loop():
+    """The one-length table lookup against the general per-(algorithm, length)
+    loop (forced by a second pair of another length that the ids do not use
+    except through the lengths list)."""
+    specs = search.job_specs(3)
+    ids = np.arange(2 * specs.per_pair)  # pairs 0 and 1 only
+    fast = specs.representative(ids, [160000, 160000, 48000])
+    specs2 = search.job_specs(3)
+    both = specs2.representative(np.arange(len(specs2)), [160000, 160000, 48000])  # loop path
+    assert np.array_equal(fast, both[:len(ids)])
+    sub = np.random.default_rng(1).choice(len(ids), 3000, replace=False)
+    assert np.array_equal(specs.representative(sub, [160000, 160000, 48000]), both[sub])
+
+
+@pytest.mark.parametrize("tol", [0.0, 1e-6, 1e-2])
+def test_select_best_blocks_equal_the_tolerance_scan(tol):
+    """The block form (running maxima, records only) against the oracle's
+    sequential scan on coarse scores full of near-ties, skipped cells and NaNs."""
+    rng = np.random.default_rng(int(tol * 1e6) + 7)
+    specs = search.job_specs(3)
+    table = np.zeros((len(specs), search.NCOL))
+    for col in (1, 3):
+        table[:, col] = np.round(rng.normal(0.5, 0.05, len(specs)), 2)
+    table[:, 2] = rng.random(len(specs)) > 0.05
+    table[rng.random(len(specs)) < 0.01, 3] = np.nan
+    for obj in ("snr", "stoi"):
+        best = search.select_best(specs, table, obj, tol=tol)
+        assert list(best.items()) == list(search.select_best(list(specs), table, obj, tol=tol).items())
+        col = search.TABLE_COLUMN[obj]
+        for (pair, alg), (cid, score) in list(best.items())[::5]:
+            ids = [c for c in range(pair * specs.per_pair, (pair + 1) * specs.per_pair)
+                   if specs.algorithms[specs.alg[c]] == alg]
+            sc = [table[c, col] if table[c, 2] and table[c, col] == table[c, col] else None for c in ids]
+            w = oracle.tolerance_scan(sc, tol)
+            assert cid == (ids[w] if w >= 0 else -1)
+
+
+def test_gather_records_rejects_duplicates_and_gaps():
+    local = np.column_stack([np.arange(5, dtype=np.float64), np.ones((5, search.NCOL))])
+    assert search.gather_records(local, 5).shape == (5, search.NCOL)
+    shuffled = local[[3, 1, 4, 0, 2]]
+    assert np.array_equal(search.gather_records(shuffled, 5), search.gather_records(local, 5))
+    for bad, n in ((local[[0, 1, 1, 3, 4]], 5), (local[:4], 5), (local, 4)):
+        with pytest.raises(RuntimeError):
+            search.gather_records(bad, n)

@@ -58,7 +58,8 @@ def main():
         if prof is not None:
             import pstats
             prof.disable()
-            pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(30)
+            pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(40)
+            pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
         key = "with_stoi" if stoi else "snr_only"
         out[key] = {"s_per_sweep": float(np.median(ts)), "cells_per_s": len(specs) / float(np.median(ts))}
         if stoi:
