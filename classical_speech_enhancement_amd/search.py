@@ -554,8 +554,11 @@ def run_grid(clean, noisy, specs, compute=None, group=None, device=None, objecti
     ids = np.nonzero(rank_of == rank)[0]
     compute = compute or engine_compute
     vals = compute(clean, noisy, specs, ids) if len(ids) else np.zeros((0, NCOL))
-    local = np.concatenate([ids[:, None].astype(np.float64), vals], axis=1)
-    table = gather_records(local, len(specs), group=group, device=device)
+    if not dist_on and len(ids) == len(specs):  # one process, every cell in order: no gather
+        table = np.asarray(vals, dtype=np.float64)
+    else:
+        local = np.concatenate([ids[:, None].astype(np.float64), vals], axis=1)
+        table = gather_records(local, len(specs), group=group, device=device)
     return table, select_best(specs, table, objective)
 
 
