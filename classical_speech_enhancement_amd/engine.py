@@ -631,18 +631,29 @@ class MultiPlan:
         return out
 
 
+def structure_digest():
+    """A 128-bit hash object for plan-reuse keys: xxh3 (an order of magnitude
+    faster than blake2b on the sweep's 17-MB batch descriptions) when the
+    xxhash module is importable, blake2b otherwise."""
+    try:
+        import xxhash
+        return xxhash.xxh3_128()
+    except ImportError:
+        import hashlib
+        return hashlib.blake2b(digest_size=16)
+
+
 def spec_fingerprint(specs):
     """Digest of a spec list's structure: per cell the signal index, the
     algorithm name and the identity of its params dict (Engine.run(reuse=True))."""
-    import hashlib
     n = len(specs)
     sig = np.fromiter((s for (s, _, _) in specs), dtype=np.int64, count=n)
     pid = np.fromiter((id(p) for (_, _, p) in specs), dtype=np.int64, count=n)
     algs = {}
     aid = np.fromiter((algs.setdefault(a, len(algs)) for (_, a, _) in specs), dtype=np.int64, count=n)
-    h = hashlib.blake2b(digest_size=16)
+    h = structure_digest()
     for arr in (sig, pid, aid):
-        h.update(arr.tobytes())
+        h.update(arr)
     h.update(repr(sorted(algs.items(), key=lambda kv: kv[1])).encode())
     return h.hexdigest()
 

@@ -282,9 +282,8 @@ def engine_compute(clean, noisy, specs, ids, engine=None, align=True, stoi=True)
 
 
 def _engine_compute(eng, clean, noisy, specs, ids, align, stoi):
-    import hashlib
     import torch
-    from .engine import snr_db, spec_fingerprint
+    from .engine import snr_db, spec_fingerprint, structure_digest
     from .metrics import StoiPlan
     ids = np.asarray(ids, dtype=np.int64)
     lengths = [len(x) for x in noisy]
@@ -297,7 +296,8 @@ def _engine_compute(eng, clean, noisy, specs, ids, align, stoi):
         pair_of = np.fromiter((specs[c][0] for c in comp), dtype=np.int64, count=len(comp))
     vals = np.full((len(comp), NCOL), np.nan)
     by_len = OrderedDict()
-    for pair in dict.fromkeys(pair_of.tolist()):  # first-appearance order
+    upairs, first = np.unique(pair_of, return_index=True)
+    for pair in upairs[np.argsort(first, kind="stable")].tolist():  # first-appearance order
         by_len.setdefault(lengths[pair], []).append(pair)
     # STOI runs on the engine's side stream: the STOI of one n_fft's cells
     # overlaps the next n_fft's enhance and alignment on the main stream
@@ -335,8 +335,9 @@ def _engine_compute(eng, clean, noisy, specs, ids, align, stoi):
         batches.append(cur)
         for pairs in batches:
             js = np.concatenate([rows[p] for p in pairs])
-            slot = {p: s for s, p in enumerate(pairs)}
-            sig = np.array([slot[p] for p in pair_of[js].tolist()], dtype=np.int64)
+            slot_of = np.full(int(max(pairs)) + 1, -1, dtype=np.int64)
+            slot_of[pairs] = np.arange(len(pairs))
+            sig = slot_of[pair_of[js]]  # the batch slot of each cell's pair
             nz = torch.as_tensor(np.stack([np.asarray(noisy[p], np.float64) for p in pairs])).cuda()
             cl = torch.as_tensor(np.stack([np.asarray(clean[p], np.float64) for p in pairs])).cuda()
             cpow = np.array([float(np.dot(np.asarray(clean[p], np.float64),
@@ -369,9 +370,9 @@ def _engine_compute(eng, clean, noisy, specs, ids, align, stoi):
             if js_specs:
                 # batches of the same structure reuse one device plan: the key
                 # is the cells' (slot, algorithm, grid cell) and this JobSpecs
-                h = hashlib.blake2b(digest_size=16)
+                h = structure_digest()
                 for arr in (sig, specs.alg[comp[js]], specs.cell[comp[js]]):
-                    h.update(np.ascontiguousarray(arr, dtype=np.int64).tobytes())
+                    h.update(np.ascontiguousarray(arr, dtype=np.int64))
                 key = ("jobspecs", id(specs), h.hexdigest())
                 run_specs, run_kw = sub, dict(reuse=key, keep=specs)
             else:
