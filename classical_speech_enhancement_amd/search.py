@@ -55,9 +55,12 @@ RECORD_FIELDS = ("cell_id", "sse", "snr", "finite", "stoi", "lag", "xstatus")
 TABLE_COLUMN = {"sse": 0, "snr": 1, "finite": 2, "stoi": 3, "lag": 4,
                 "xstatus": 5}  # table = records without cell_id
 NCOL = len(RECORD_FIELDS) - 1
-# bound on the cell waveforms held at once for STOI scoring (f32 bytes): 32 GB
-# of the 288 GB HBM, i.e. 5 full 10-s pairs (9,744 cells x 640 KB each) per batch
-STOI_WAVE_BYTES = 32 << 30
+# bound on the cell waveforms held at once for STOI scoring (f32 bytes): 48 GiB
+# of the 288 GB HBM, i.e. 10 full 10-s pairs (7,308 computed cells x 640 KB each)
+# per batch, two batches in flight.  100-pair sweep (late r04, tools/call_r04s.sh):
+# 16 GiB 1.48-1.49 s, 32 GiB 1.31-1.32 s, 48 GiB 1.256-1.258 s, 64 GiB
+# 1.253-1.295 s; 96 GiB ran out of memory
+STOI_WAVE_BYTES = 48 << 30
 
 
 class JobSpecs(list):
@@ -264,7 +267,7 @@ def engine_compute(clean, noisy, specs, ids, engine=None, align=True, stoi=True)
     Device memory: an engine made here is dropped with its cached plans on
     return.  A caller's engine keeps its plan_cache_size; the STOI path holds
     two plans while it runs (double-buffered waveforms: 2 x STOI_WAVE_BYTES =
-    64 GB peak plus each plan's analysis buffers) and trims the cache back to
+    96 GiB peak plus each plan's analysis buffers) and trims the cache back to
     the caller's size on return."""
     from .engine import Engine
     own = engine is None

@@ -30,7 +30,11 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--profile", action="store_true", help="cProfile the timed STOI sweeps (host side)")
+    ap.add_argument("--wave-gb", type=float, default=None,
+                    help="override search.STOI_WAVE_BYTES (GiB of cell waveforms per STOI batch)")
     a = ap.parse_args()
+    if a.wave_gb is not None:
+        search.STOI_WAVE_BYTES = int(a.wave_gb * (1 << 30))
     import torch
     pairs = [make_pair(200 + i, a.seconds) for i in range(a.pairs)]
     clean = [c for c, _ in pairs]
