@@ -78,3 +78,20 @@ def test_on_plan_reaches_the_plan():
     got = []
     eng.run(X, [("a",)], reuse="A", on_plan=got.append)
     assert len(got) == 1
+
+
+def test_structure_digest_and_fingerprint():
+    """Plan-reuse keys: the digest object hashes numpy buffers without a copy
+    (xxh3 when importable, blake2b otherwise) and equal structures give equal
+    fingerprints, different ones different."""
+    import numpy as np
+    from classical_speech_enhancement_amd.engine import spec_fingerprint, structure_digest
+    a, b = structure_digest(), structure_digest()
+    x = np.arange(1000, dtype=np.int64)
+    a.update(x)
+    b.update(x.tobytes())
+    assert a.hexdigest() == b.hexdigest() and len(a.hexdigest()) == 32
+    p, q = {"n_fft": 512}, {"n_fft": 1024}
+    s1 = [(0, "wiener", p), (1, "mmse", q)]
+    assert spec_fingerprint(s1) == spec_fingerprint(list(s1))
+    assert spec_fingerprint(s1) != spec_fingerprint([(0, "wiener", p), (1, "mmse", p)])
