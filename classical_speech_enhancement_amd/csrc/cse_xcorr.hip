@@ -55,8 +55,10 @@ template <int PAD>
 __device__ __forceinline__ int pxl(int p) { return p + (PAD == 16 ? (p >> 4) : (p >> 5)); }
 __device__ __forceinline__ int px(int p) { return pxl<32>(p); }
 constexpr int XR = XH / 16 + XH / 16 / 32;  // px32 stride of 256 points: 264
+// __launch_bounds__' second argument is waves per SIMD; with XT = 256 (one wave
+// per SIMD per workgroup) that equals workgroups per CU
 #ifndef CSE_XC_WG_PER_CU
-#define CSE_XC_WG_PER_CU 3    // 168 VGPRs + 72 B spill: 4% faster than 2 (192, no spill); 4 spills 240 B
+#define CSE_XC_WG_PER_CU 3   // 168 VGPRs + 72 B spill: 4% faster than 2 (192, no spill); 4 spills 240 B
 #endif
 
 // one radix-16 Stockham pass of stride NS (compile-time, so every padded
