@@ -55,7 +55,11 @@ sys.path.insert(0, REPO)
 METRIC = ("STFT frame-gain evals/sec/node, 16kHz 512-pt FFT full grid; 1/2/4/8-GPU scaling")
 HBM_PEAK = 8.0e12              # MI355X_MICROARCH.md: 8.0 TB/s spec
 SIMDS = 1024                   # 256 CUs x 4 SIMD-32
-DENSE_VALU_CYC, DENSE_TRANS_CYC = 2.71, 4.86  # tools/micro/valu_peak.hip, 8 waves/SIMD
+# what a dense, dependency-free VALU stream sustains per SIMD, in shader cycles
+# per wave-instruction (tools/micro/valu_peak.hip, profiles/r05_micro_valu_peak.txt),
+# by waves per SIMD: {waves: (v_fma_f32, v_pk_fma_f32, v_exp_f32)}
+DENSE_CYC = {3: (4.06, 3.94, 6.64), 4: (3.46, 3.31, 5.75), 8: (2.71, 2.64, 4.86)}
+FP32_PEAK = 157.3e12           # MI355X_MICROARCH.md: FP32 vector, spec
 VALU_CYC, TRANS_CYC = 2, 4     # wave64 issue cycles: v_fma_f32 (SIMD-32), transcendental (2x: tools/micro/valu_rate.hip)
 CLOCK = 2.4e9                  # max shader clock
 TOL = 1e-5                     # north-star relative waveform tolerance
@@ -640,20 +644,29 @@ def main():
 def roofline_block(n_fft, units, kern_ms):
     """The enhance kernel against the resource it spends: VALU issue.
 
-    achieved = the launch's SIMD issue cycles (PMC instruction counts of this
-    binary and launch: VALU 2 cycles per wave64, transcendental 4, fp64 FMA/MUL/
-    ADD 4) / the live HIP-event kernel time; peak = 1024 SIMDs x 2.4 GHz.
-    frac_at_held_clock uses the clock the profiled run held instead.  Beside
-    it: the measured HBM traffic (PMC) as GB/s, and SURVEY §8(d)'s nominal
-    12 B/bin (read P, read N, write G) as a byte count only: the fused kernel
-    never writes G and reads the shared rows once per 16-cell workgroup, so
-    those bytes are not moved and are not a bandwidth (as a rate they would
-    exceed the HBM peak); `pmc_traffic_over_nominal` says how much of them
-    the launch really moves."""
+    The product binary's own instruction counts (PMC of this launch size and
+    n_fft, committed under profiles/ and matched to this build by a digest of
+    the kernel sources and flags): `achieved` = its issue cycles (wave64 f32
+    VALU 2 cycles on a SIMD-32, a packed v_pk_* instruction too: it issues at
+    the scalar rate, tools/micro/valu_peak.hip; transcendental 4) / the live
+    HIP-event kernel time; `peak` = 1024 SIMDs x 2.4 GHz.  Beside it:
+      dense_at_occupancy  the same counts priced at what a dependency-free
+                          VALU stream sustains at the kernel's own waves per
+                          SIMD (tools/micro/valu_peak.hip): how much of the
+                          issue shortfall occupancy alone explains;
+      fp32_flops          SQ_INSTS_VALU_FLOPS_FP32 (per wave-instruction,
+                          weighted by the FLOPs of each lane: x 64) against the
+                          157.3 TF FP32 vector peak;
+      traffic             the measured HBM bytes (PMC) and SURVEY 8(d)'s
+                          nominal 12 B/bin (read P, read N, write G) as a byte
+                          count only: the fused kernel never writes G and reads
+                          the shared rows once per 16-cell workgroup, so those
+                          bytes are not moved and are not a bandwidth."""
     bytes_per_unit = 12 * (n_fft // 2 + 1)
     ks = kern_ms / 1e3
     nominal = units * bytes_per_unit
-    roof = {"bound": "valu", "achieved": None, "peak": SIMDS * CLOCK / 1e9,
+    roof = {"bound": "valu issue (latency / occupancy-limited)", "achieved": None,
+            "peak": SIMDS * CLOCK / 1e9,
             "unit": "G SIMD issue-cycles/s (1024 SIMDs)", "frac": None, "traffic": None,
             "kernel": f"cse::enhance_kernel<{n_fft}>", "kernel_ms": kern_ms,
             "units_per_launch": units,
@@ -681,30 +694,35 @@ def roofline_block(n_fft, units, kern_ms):
         roof["hbm_measured_GBps"] = tb / ks / 1e9
         roof["hbm_measured_frac"] = tb / ks / HBM_PEAK
         roof["pmc_traffic_over_nominal"] = tb / nominal
-    need = pmc.get("valu_issue_cycles")
-    if need:
+    vi, tr = pmc.get("sq_insts_valu"), pmc.get("sq_insts_valu_trans")
+    if vi and tr is not None:
+        need = VALU_CYC * (vi - tr) + TRANS_CYC * tr
         roof["achieved"] = need / ks / 1e9
         roof["frac"] = need / ks / (SIMDS * CLOCK)
         roof["issue_cycles_per_launch"] = need
-        roof["cycles_per"] = ("wave64 VALU 2, transcendental 4 (tools/micro/valu_rate.hip), "
-                              "fp64 FMA/MUL/ADD 4 per SIMD")
-        if pmc.get("clock_ghz_profiled"):
-            roof["clock_ghz_profiled"] = pmc["clock_ghz_profiled"]
-            roof["frac_at_held_clock"] = pmc.get("valu_frac")
-        if pmc.get("valu_issue_cycles_source"):
-            roof["issue_cycles_source"] = pmc["valu_issue_cycles_source"]
-        # the same instruction counts priced at what a dense independent stream
-        # sustains on the part (tools/micro/valu_peak.hip, 8 waves/SIMD, shader
-        # cycles from s_memtime: v_fma_f32 2.71, v_exp_f32 4.86 per wave-
-        # instruction; profiles/r04_micro_valu_peak.txt) at the profiled clock:
-        # how close the kernel runs to a VALU stream with no dependencies, LDS or
-        # barriers at all, rather than to the datasheet's 2 cycles
-        vi, tr = pmc.get("valu_insts_scalar_equiv"), pmc.get("trans_insts")
-        if vi and tr is not None and pmc.get("clock_ghz_profiled"):
-            dense = DENSE_VALU_CYC * (vi - tr) + DENSE_TRANS_CYC * tr
-            roof["dense_stream_cycles"] = dense
-            roof["frac_vs_dense_stream"] = dense / (SIMDS * pmc["clock_ghz_profiled"] * 1e9 * ks)
-        for k in ("share_wait_inst_any", "lds_conflict_cycles_per_lds_inst", "vgprs"):
+        roof["cycles_per"] = ("wave64 VALU 2 (packed v_pk_* too), transcendental 4 per SIMD; "
+                              "this binary's own SQ_INSTS_VALU / _TRANS_F32")
+        clk = pmc.get("clock_ghz_profiled")
+        if clk:
+            roof["clock_ghz_profiled"] = clk
+            roof["frac_at_held_clock"] = need / ks / (SIMDS * clk * 1e9)
+        w = pmc.get("waves_per_simd")
+        if w in DENSE_CYC and clk:
+            fma, _, exp = DENSE_CYC[w]
+            dense = fma * (vi - tr) + exp * tr
+            roof["dense_at_occupancy"] = {
+                "waves_per_simd": w, "cycles_per_valu": fma, "cycles_per_trans": exp,
+                "frac": dense / (SIMDS * clk * 1e9 * ks),
+                "source": "tools/micro/valu_peak.hip (profiles/r05_micro_valu_peak.txt)"}
+        fl = pmc.get("sq_insts_valu_flops_fp32")
+        if fl:
+            roof["fp32_flops"] = {"achieved_TFLOPs": fl * 64 / ks / 1e12,
+                                  "peak_TFLOPs": FP32_PEAK / 1e12,
+                                  "frac": fl * 64 / ks / FP32_PEAK,
+                                  "counter": ("SQ_INSTS_VALU_FLOPS_FP32 x 64: the counter counts per "
+                                              "wave-instruction, weighted by FLOPs per lane")}
+        for k in ("share_wait_inst_any", "share_wait_any", "lds_conflict_cycles_per_lds_inst",
+                  "vgprs", "waves_per_simd"):
             if pmc.get(k) is not None:
                 roof[k] = pmc[k]
     return roof

@@ -312,4 +312,24 @@ __device__ __forceinline__ void idft16_pk(f2 (&v)[16]) {
     for (int i = 0; i < 16; ++i) v[i] = t[i];
 }
 
+// In-register inverse DFT of length 8 on packed complex values (sign +i):
+// radix-2 over the even / odd inputs, x[s] = E[s] + W8^s O[s], x[s + 4] =
+// E[s] - W8^s O[s] with W8 = e^{2πi/8}: W8^1 O = r2 (o.x - o.y, o.x + o.y),
+// W8^2 O = i O, W8^3 O = r2 (-o.x - o.y, o.x - o.y); 26 instructions.
+__device__ __forceinline__ void idft8_pk(f2 (&v)[8]) {
+    constexpr float r2 = 0.70710678118654752f;
+    idft4_pk(v[0], v[2], v[4], v[6]);  // E[0..3] in v[0], v[2], v[4], v[6]
+    idft4_pk(v[1], v[3], v[5], v[7]);  // O[0..3] in v[1], v[3], v[5], v[7]
+    const f2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+    const f2 o0 = v[1], o1 = p_rot1(v[3]), o2 = v[5], o3 = p_rot3(v[7]);
+    v[0] = e0 + o0;
+    v[4] = e0 - o0;
+    v[1] = pfma(pdup(r2), o1, e1);
+    v[5] = pfma(-pdup(r2), o1, e1);
+    v[2] = p_addi(e2, o2);
+    v[6] = p_subi(e2, o2);
+    v[3] = pfma(pdup(r2), o3, e3);
+    v[7] = pfma(-pdup(r2), o3, e3);
+}
+
 }  // namespace cse

@@ -37,6 +37,17 @@
 #ifndef CSE_ROT_TABLE_1024
 #define CSE_ROT_TABLE_1024 0  // 1024: packing rotors as base x W32^j (the table measured slower)
 #endif
+#ifndef CSE_SPLIT_T
+#define CSE_SPLIT_T 0  // n_fft 512 sweep kernel: pass 2 through a half block (see WG::SPLIT)
+#endif
+#ifndef CSE_NAT_Y
+#define CSE_NAT_Y 0
+#endif
+#ifndef CSE_DMA_ROWS
+#define CSE_DMA_ROWS 0  // n_fft 512 (packed, OUT = false): rows by LDS-DMA, staged at frame end
+#endif
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 namespace cse {
 
@@ -189,6 +200,13 @@ __device__ __forceinline__ float gain_omlsa(float gam2, float dd, float& rr, flo
     return G;
 }
 
+// The reference's skip of a cell (speech_enhancement_comparison.py:102-103) as
+// this kernel reports it: a slot that breaks the slot-group contract (cse.h)
+__device__ __forceinline__ void reject_cell(const Args& a, int64_t c) {
+    if (a.sse) a.sse[c] = __builtin_nan("");
+    if (a.finite) a.finite[c] = 0;
+}
+
 // ---------------------------------------------------------------------------
 // Block -> slot-group order.  Blocks are dealt round-robin over the 8 XCDs
 // (block b runs on XCD b % 8, as its (b/8)-th block there), and the host sorts
@@ -214,13 +232,40 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 // SS), clean[retired samples]) into LDS once, cooperatively, one frame ahead
 // (a few VGPRs per thread).
 // ---------------------------------------------------------------------------
-template <int NFFT>
+template <int NFFT, bool OUT = false>
 struct WG {
     using G = Geo<NFFT>;
     static constexpr int WAVES = NFFT == 512 ? CSE_WG_WAVES : CSE_WG_WAVES_1024;
     static constexpr int THREADS = 64 * WAVES;
     static constexpr int CPWG = WAVES * G::CPW;                   // cells per workgroup
     static constexpr int HMAX = 256;                              // largest hop
+    // shared rows (double-buffered): Y (float2 [B]); G (float [B], or the
+    // (gamma, d) / (N, P) float2 [B] at 512); A (float [B], 512: MMSE's
+    // c/(gamma + 1e-12), SS's 1/|Y|); clean (float [HMAX])
+    static constexpr bool R2 = (NFFT == 512);
+    // packed pairs (CSE_PK): the rows in mirror-pair order, 16-B records
+    static constexpr bool PK = R2 ? CSE_PK : CSE_PK_1024;
+    // Rows by LDS-DMA (global_load_lds, no VGPR destination; the n_fft 512
+    // sweep kernel): every wave loads its quarter of frame t+1's Y row (natural
+    // bin order, the double-buffered row the gain stage reads), of the noise row
+    // and of the clean samples at the start of frame t, and stages its own
+    // quarter of the derived rows (gamma/d or gamma/cig records, the clean row)
+    // at the end of frame t, after its own vmcnt(0): the loads are in flight
+    // for a whole frame and hold no registers (r04 held 8 VGPRs of prefetched
+    // rows through every frame).  The OUT variant (gain matrices, tests) keeps
+    // register staging and the pair-order Y / A rows.
+    static constexpr bool DMA = R2 && PK && CSE_DMA_ROWS && !OUT;
+    // natural-order Y rows and MMSE's cig in the G record's d slot (DMA, or
+    // register staging with CSE_NAT_Y: experiments)
+    static constexpr bool NAT = DMA || (R2 && PK && CSE_NAT_Y && !OUT);
+    // Pass 2 through half a transpose block (n_fft 512 sweep kernel): rows
+    // b < 8 of the 16 x 16 block, then rows b >= 8, each lane reading half a
+    // row; lanes i and i ^ 8 (one DPP row of the cell) finish the first
+    // radix-2 step of the DFT16 over the columns with a row_ror:8 exchange and
+    // own the even / odd outputs of rows i & 7 and (i & 7) + 8 (two DFT8s).
+    // The per-cell region shrinks from 2,176 to the exchange slots' 1,152 B
+    // (16 cells: 34.8 -> 18.4 KB of LDS), with no register more in flight.
+    static constexpr bool SPLIT = R2 && PK && CSE_SPLIT_T && !OUT;
     // per-cell LDS region: the mirror-exchange slots (9 complex per lane,
     // stride 72 B: the 16 lanes of a ds_write_b64 group hit disjoint banks)
     // aliased with the transpose block (16 rows x TS = L + 1 complex).  Its
@@ -232,16 +277,12 @@ struct WG {
     static constexpr int TB = 16 * TS * 8;
     static constexpr int CREG_RAW = XB > TB ? XB : TB;
     static constexpr int CREG_U = (CREG_RAW + 127) / 128;
-    static constexpr int CREG = (CREG_U + (CREG_U % 2 ? 0 : 1)) * 128;
-    // shared rows (double-buffered): Y (float2 [B]); G (float [B], or the
-    // (gamma, d) / (N, P) float2 [B] at 512); A (float [B], 512: MMSE's
-    // c/(gamma + 1e-12), SS's 1/|Y|); clean (float [HMAX])
-    static constexpr bool R2 = (NFFT == 512);
-    // packed pairs (CSE_PK): the rows in mirror-pair order, 16-B records
-    static constexpr bool PK = R2 ? CSE_PK : CSE_PK_1024;
+    static constexpr int CREG = SPLIT ? XB : (CREG_U + (CREG_U % 2 ? 0 : 1)) * 128;
+    static constexpr int TS2 = 17;  // SPLIT: row stride (complex) of the half block
+    static_assert(!SPLIT || (8 * TS2 * 8 <= XB && XB % 256 == 128), "half block in the exchange slots");
     static constexpr int YROW = ((G::B * 8 + 15) / 16) * 16;      // bytes of one Y row
     static constexpr int GROW = ((G::B * (R2 ? 8 : 4) + 15) / 16) * 16;
-    static constexpr int AROW = R2 ? ((G::B * 4 + 15) / 16) * 16 : 0;
+    static constexpr int AROW = (R2 && !DMA) ? ((G::B * 4 + 15) / 16) * 16 : 0;
     static constexpr int OFF_Y = CPWG * CREG;                     // float2[2][B] (double buffer)
     static constexpr int OFF_G = OFF_Y + 2 * YROW;
     static constexpr int OFF_A = OFF_G + 2 * GROW;
@@ -279,24 +320,35 @@ struct WG {
     static constexpr int WSLOTS = HALF_TABLES ? 16 : 32;
     static constexpr int WSTR = HALF_TABLES ? 20 : 36;
     static constexpr int OFF_WIN = OFF_CP + CPWG * 32;
-    static constexpr int BYTES = OFF_WIN + G::L * WSTR * 4;
+    // DMA: the landing rows of the noise (f32 [B]) and of the clean samples (f64 [HMAX]),
+    // each wave's quarter its own
+    static constexpr int OFF_RN = OFF_WIN + G::L * WSTR * 4;
+    static constexpr int RNB = DMA ? ((G::B * 4 + 15) / 16) * 16 : 0;
+    static constexpr int OFF_RC = OFF_RN + RNB;
+    // SPLIT: the odd-output twiddles W16^c (c = 1..7) of lanes i >= 8, (1, 0)
+    // for lanes i < 8 (branch-free, VGPR operands: as SGPR pairs of constants
+    // the twiddles spilled 90 SGPRs), a row of 8 complex per lane, stride 80 B
+    static constexpr int OFF_T2 = OFF_RC + (DMA ? HMAX * 8 : 0);
+    static constexpr int BYTES = OFF_T2 + (SPLIT ? G::L * 80 : 0);
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
-// the registers (3 waves/SIMD) set the occupancy: LDS must not cut it below
-// 12 waves (3 per SIMD) per CU
-static_assert((163840 / WG<512>::BYTES) * WG<512>::WAVES >= 12,
+// waves per SIMD the register allocation targets (VGPR budget 512 / w)
+#ifndef CSE_WAVES_PER_SIMD
+#define CSE_WAVES_PER_SIMD 3
+#endif
+
+// the registers set the occupancy: LDS must not cut it below CSE_WAVES_PER_SIMD
+// (the sweep kernels) or 3 (the OUT variants) waves per SIMD
+static_assert((163840 / WG<512, false>::BYTES) * WG<512, false>::WAVES >= 4 * CSE_WAVES_PER_SIMD,
+              "n_fft=512 sweep workgroups must fit the register occupancy");
+static_assert((163840 / WG<512, true>::BYTES) * WG<512, true>::WAVES >= 12,
               "n_fft=512 workgroups must fit 12 waves per CU");
 static_assert((163840 / WG<1024>::BYTES) * WG<1024>::WAVES >= 12,
               "n_fft=1024 workgroups must fit 12 waves per CU");
 static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
               WG<1024>::CPWG == CSE_CELLS_PER_GROUP(1024), "cse.h slot-group size");
 
-// waves per SIMD the register allocation targets (VGPR budget 512 / w)
-
-#ifndef CSE_WAVES_PER_SIMD
-#define CSE_WAVES_PER_SIMD 3
-#endif
 
 // Ordering of LDS accesses between the lanes of ONE wave: the LDS executes a
 // wave's DS instructions in issue order, so a compiler-level barrier is all a
@@ -354,7 +406,9 @@ __device__ __forceinline__ float gain_bin(float2& y, RowV rv, float& rr, float a
         const float pz = fmaf(yx, yx, yy * yy);
         const float u = sp * __builtin_amdgcn_rsqf(pz);
         g = (pz > 0.0f) ? u * sc : 0.0f;
-        y = (pz > 0.0f) ? make_float2(yx, yy) : make_float2(1.0f, 0.0f);  // angle(0) = 0
+        // angle(0) = 0; a NaN/inf spectrum value keeps the NaN phase np.angle gives it
+        y = (pz > 0.0f) ? make_float2(yx, yy)
+                        : (pz == 0.0f ? make_float2(1.0f, 0.0f) : make_float2(pz - pz, pz - pz));
         return (pz > 0.0f) ? u : sp;
     }
     // dd = (1 - alpha_t) max(gamma - 1, 0): at 512 d is the stager's row; at 1024
@@ -470,7 +524,7 @@ __device__ __forceinline__ f2 gain_pair(f2 gam, f2 d, f2 a, f2& rr, float alpha_
 // records (Y_p, Y_{M-p}) (16 B); at 512 (g_p, g_{M-p}, d_p, d_{M-p}) (16 B) and
 // MMSE's / SS's a pairs (8 B), at 1024 (g_p, g_{M-p}) (8 B).  Packing rotors:
 // the lane's table row (512) or base x W32^j (1024).
-template <int NFFT, int ALGO, bool OUT>
+template <int NFFT, int ALGO, bool OUT, bool NAT = false>
 __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
                                              const void* __restrict__ growv,
                                              const float2* __restrict__ a2row, f2 (&z)[16],
@@ -481,8 +535,21 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
                                              float* __restrict__ gout_row, int i) {
     constexpr int L = Geo<NFFT>::L, M = Geo<NFFT>::M;
     constexpr bool R2 = (NFFT == 512);
-    constexpr bool WANT_A = R2 && (ALGO == CSE_ALGO_MMSE || (ALGO == CSE_ALGO_SS && OUT));
+    constexpr bool WANT_A = R2 && !NAT && (ALGO == CSE_ALGO_MMSE || (ALGO == CSE_ALGO_SS && OUT));
     const float4* y4 = y4row + i;
+    // NAT (DMA rows): Y in natural bin order, bins k = i + L j and M - k read
+    // as two 8-byte records; the G record's d slot holds MMSE's
+    // (sqrt(pi)/2)/(gamma + 1e-12) and d = max(gamma - 1, 0) is formed here
+    const float2* ylo = (const float2*)y4row + i;
+    const float2* yhi = (const float2*)y4row + (M - i);
+    auto ldy = [&](int k) {  // the pair record of pair index k (NAT: two reads)
+        if constexpr (NAT) {
+            const float2 a = ylo[k], b = yhi[-k];
+            return make_float4(a.x, a.y, b.x, b.y);
+        } else {
+            return y4[k];
+        }
+    };
     const float4* g4 = (const float4*)growv + i;  // 512
     const float2* g2 = (const float2*)growv + i;  // 1024
     const float2* a2 = a2row + i;
@@ -492,14 +559,15 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
         const float2 v = g2[k];
         return make_float4(v.x, v.y, 0.0f, 0.0f);
     };
-    float4 yc = y4[0], gc = ldg(0);
+    float4 yc = ldy(0), gc = ldg(0);
     float2 ac = WANT_A ? a2[0] : make_float2(0.0f, 0.0f);
     const cf base = R2 ? cmk(1.0f, 0.0f) : *base_p;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         // next pair's rows (j = 7: bin M/2, the record of pair M/2)
         const int nx = (j < 7) ? L * (j + 1) : M / 2 - i;
-        const float4 yn = y4[nx], gn = ldg(nx);
+        const float4 yn = (NAT && j == 7) ? make_float4(ylo[nx].x, ylo[nx].y, 0.0f, 0.0f) : ldy(nx),
+                     gn = ldg(nx);
         const float2 an = WANT_A ? a2[nx] : make_float2(0.0f, 0.0f);
         f2 ya = f2{yc.x, yc.y}, yb = f2{yc.z, yc.w};
         f2 g;  // the pair's gains
@@ -514,7 +582,15 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
             ya = f2{y0.x, y0.y};  // 1024: the rescaled phasor source where Y is tiny
             yb = f2{y1.x, y1.y};
         } else {
-            g = gain_pair<NFFT, ALGO>(f2{gc.x, gc.y}, f2{gc.z, gc.w}, f2{ac.x, ac.y}, rr[j], alpha_t, cpar);
+            if (NAT && ALGO == CSE_ALGO_MMSE) {  // record (gamma pair, cig pair)
+                const f2 gam = f2{gc.x, gc.y};
+                const f2 dm = gam - 1.0f;
+                g = gain_pair<NFFT, ALGO>(gam, f2{fmaxf(dm.x, 0.0f), fmaxf(dm.y, 0.0f)},
+                                          f2{gc.z, gc.w}, rr[j], alpha_t, cpar);
+            } else {
+                g = gain_pair<NFFT, ALGO>(f2{gc.x, gc.y}, f2{gc.z, gc.w}, f2{ac.x, ac.y}, rr[j],
+                                          alpha_t, cpar);
+            }
             s = g;
         }
         if (OUT && gout_row) {
@@ -546,7 +622,9 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
     // bin M/2: scalar, Z'[M/2] = 2 conj(X_{M/2})
     float2 ym = make_float2(yc.x, yc.y);
     float gm;
-    const float sm = 2.0f * gain_bin<NFFT, ALGO>(ym, RowV{gc.x, gc.z, ac.x}, rrm, alpha_t, cpar, gm);
+    const RowV rvm = (NAT && ALGO == CSE_ALGO_MMSE) ? RowV{gc.x, fmaxf(gc.x - 1.0f, 0.0f), gc.z}
+                                                    : RowV{gc.x, gc.z, ac.x};
+    const float sm = 2.0f * gain_bin<NFFT, ALGO>(ym, rvm, rrm, alpha_t, cpar, gm);
     if (OUT && gout_row && i == 0) gout_row[M / 2] = gm;
     xw[8] = f2{ym.x * sm, -ym.y * sm};
 }
@@ -674,11 +752,35 @@ __device__ __forceinline__ void gain_pack(const float2* __restrict__ yrow,
     xw[8] = cmk(ya.x * sm, -ya.y * sm);
 }
 
+// Position inside a frame (relative to the lane's first sample) of the lane's
+// output slot q: the pass-2 DFT16 gives lane b2 the samples 2 b2 + 32 p + e
+// (slot q = 2 p + e); the split pass 2 gives lane i = 8 h + l the samples
+// 2 l + 32 h + 16 r + 64 s + e of rows l + 8 r (slot q = 4 s + 2 r + e).  Either
+// way slot q + F lies HOP samples after slot q.
+template <bool SPLIT, int SP>
+__device__ __forceinline__ constexpr int slot_pos(int q) {
+    return SPLIT ? 64 * (q >> 2) + 16 * ((q >> 1) & 1) + (q & 1) : SP * (q >> 1) + (q & 1);
+}
+
+// The eight (hop, algorithm) bodies as separate functions (CSE_RUNWG_NOINLINE,
+// the n_fft 512 unit at 4 waves/SIMD): inlined into one kernel, the compiler
+// hoisted every body's constants to the entry and the union spilled 160
+// VGPRs and 70 SGPRs at the 128-VGPR cap; as callees each body is allocated
+// on its own (one call per workgroup)
+#ifndef CSE_RUNWG_NOINLINE
+#define CSE_RUNWG_NOINLINE 0
+#endif
+#if CSE_RUNWG_NOINLINE
+#define CSE_RUNWG_ATTR __noinline__
+#else
+#define CSE_RUNWG_ATTR __forceinline__
+#endif
+
 template <int NFFT, int HOP, int ALGO, bool OUT>
-__device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, int n_cells_wg,
+__device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, int n_cells_wg,
                                        unsigned char* smem) {
     using G = Geo<NFFT>;
-    using W = WG<NFFT>;
+    using W = WG<NFFT, OUT>;
     constexpr int M = G::M, L = G::L, B = G::B, SP = G::SP, MH = M / 2;
     constexpr int R = NFFT / HOP;       // frames overlapping one sample
     constexpr int F = 2 * HOP / SP;     // samples a lane retires per frame
@@ -704,8 +806,20 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     const int need = (len + NFFT + HOP - 1) / HOP;
     const int nf = need < T ? need : T;
 
-    // ---- my cell
-    const bool valid = cslot < n_cells_wg && wcell[cslot].algo == ALGO;
+    // ---- my cell.  The slot group's shared rows are slot 0's; a slot whose
+    // shared fields differ from slot 0's (cse.h: algo, hop, y_offset,
+    // noise_offset, noise_stride, clean_offset, lag) is not computed: it gets
+    // the reference's skip (finite = 0, sse = NaN), written here, never
+    // uninitialised outputs.  Padding slots (CSE_ALGO_NONE) write nothing.
+    bool valid = false;
+    if (cslot < n_cells_wg && wcell[cslot].algo != CSE_ALGO_NONE) {
+        const cse_cell_t* me = wcell + cslot;
+        valid = me->algo == ALGO && me->hop == HOP && me->y_offset == wcell[0].y_offset &&
+                me->noise_offset == wcell[0].noise_offset &&
+                me->noise_stride == wcell[0].noise_stride &&
+                me->clean_offset == wcell[0].clean_offset && me->lag == wcell[0].lag;
+        if (!valid && i == 0) reject_cell(a, (int64_t)(me - a.cells));
+    }
     // waveform output (any variant) and gain output (OUT variant only)
     const bool want_y = a.y_out != nullptr;  // uniform
     const int out_len = (int)a.out_len;
@@ -745,19 +859,31 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     for (int e = tid; e < L * 32; e += W::THREADS) {
         const int ii = e / 32, q = e % 32;
         const int bb = (L == 16) ? ii : (ii & 15), hh = (L == 16) ? 0 : (ii >> 4);
-        const int n = SP * (q >> 1) + 2 * bb + 32 * hh + (q & 1);
+        const int n = (W::SPLIT ? 2 * (ii & 7) + 32 * (ii >> 3) : 2 * bb + 32 * hh) +
+                      slot_pos<W::SPLIT, SP>(q);
         const double w = 0.5 - 0.5 * cospi(2.0 * (double)n / (double)NFFT);
         double S = 0.0;
         for (int m = n % HOP; m < NFFT; m += HOP) {
             const double wm = 0.5 - 0.5 * cospi(2.0 * (double)m / (double)NFFT);
             S += wm * wm;
         }
-        if (q < W::WSLOTS) ((float*)(smem + W::OFF_WIN))[ii * W::WSTR + q] = (float)(w / (NFFT * S));
+        // SPLIT: lanes i >= 8 hold the negated odd outputs (see pass 2); their
+        // window entries carry the sign back
+        const double wn = (W::SPLIT && (ii & 8)) ? -w : w;
+        if (q < W::WSLOTS) ((float*)(smem + W::OFF_WIN))[ii * W::WSTR + q] = (float)(wn / (NFFT * S));
         if (W::ROT_TABLE ? q < 8 : q == 0) {
             double sn, cn;
             sincospi(2.0 * (double)(ii + L * q) / (double)NFFT, &sn, &cn);
             ((cf*)(smem + W::OFF_LC + (W::ROT_TABLE ? W::ROTSTR : 8) * ii))[q] =
                 cmk((float)cn, (float)sn);
+        }
+    }
+    if constexpr (W::SPLIT) {
+        for (int e = tid; e < L * 8; e += W::THREADS) {
+            const int ii = e >> 3, c = e & 7;
+            double sn = 0.0, cn = 1.0;
+            if (ii & 8) sincospi((double)c / 8.0, &sn, &cn);  // W16^c = e^{2πi c/16}
+            ((cf*)(smem + W::OFF_T2 + 80 * ii))[c] = cmk((float)cn, (float)sn);
         }
     }
     for (int c = tid; c < W::CPWG; c += W::THREADS) {
@@ -796,6 +922,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     // compiler wait (vmcnt(0)) for every row load right after issuing them
     double pc[W::CPT];
     auto load_rows = [&](int t) {  // issue loads of frame t's rows into registers
+        if constexpr (W::DMA) return;
         if (t < nf) {
 #pragma unroll
             for (int u = 0; u < W::YPT; ++u) {
@@ -819,6 +946,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     // phasor of Y in place of Y and 1/|Y| (gain output) — computed once here
     // for the workgroup's cells instead of by each of them
     auto store_rows = [&](int t) {  // registers -> LDS rows of frame t
+        if constexpr (W::DMA) return;
         if (t < nf) {
             float2* yrow = (float2*)(smem + W::OFF_Y + (t & 1) * W::YROW);
             float* grow = (float*)(smem + W::OFF_G + (t & 1) * W::GROW);
@@ -835,7 +963,10 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                     const int pp = k <= M / 2 ? k : M - k, hh = k <= M / 2 ? 0 : 1;
                     auto put = [&](float2 yv, float gv, float dv) {
                         if constexpr (W::PK) {
-                            yrow[2 * pp + hh] = yv;
+                            if constexpr (W::NAT)
+                                yrow[k] = yv;
+                            else
+                                yrow[2 * pp + hh] = yv;
                             grow[4 * pp + hh] = gv;
                             grow[4 * pp + 2 + hh] = dv;
                         } else {
@@ -856,12 +987,20 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                         const float yx = y.x * sc, yy = y.y * sc;
                         const float pz = fmaf(yx, yx, yy * yy);
                         const float r = __builtin_amdgcn_rsqf(pz);
-                        put(pz > 0.0f ? make_float2(yx * r, yy * r) : make_float2(1.0f, 0.0f), pn[u], P);
+                        // (1, 0) where y = 0 (angle(0) = 0); NaN where y is not
+                        // finite (np.angle(NaN) / of an inf is NaN or a value the
+                        // NaN |Y|^2 poisons anyway: S = sqrt(Ps) e^{i angle} is NaN)
+                        put(pz > 0.0f ? make_float2(yx * r, yy * r)
+                                      : (pz == 0.0f ? make_float2(1.0f, 0.0f)
+                                                    : make_float2(pz - pz, pz - pz)),
+                            pn[u], P);
                         if (OUT) arow[ai] = pz > 0.0f ? r * sc : 0.0f;
                     } else {
                         const float gam = fmaxf(P * pn[u], EPS);
                         // OMLSA's bins take gamma log2(e) (gain_omlsa), d from gamma
-                        put(y, ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam, fmaxf(gam - 1.0f, 0.0f));
+                        put(y, ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam,
+                            (W::NAT && ALGO == CSE_ALGO_MMSE) ? 0.88622692545275801f * fast_rcp(gam + 1e-12f)
+                                                               : fmaxf(gam - 1.0f, 0.0f));
                         if (ALGO == CSE_ALGO_MMSE)
                             arow[ai] = 0.88622692545275801f * fast_rcp(gam + 1e-12f);
                     }
@@ -875,20 +1014,135 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             if (j < HOP) crow[j] = pc[u];
         }
     };
-    if (!nstride) {
+    // ---- DMA rows (W::DMA): wave wv loads bins [64 wv, 64 wv + 64) of the Y row
+    // (into the double-buffered natural-order row the gain stage reads) and of
+    // the noise row, wave 0 also bin M, and the clean samples [wv S4, wv S4 +
+    // S4) (f64, as dword pairs; indices clamped into the signal, the stager
+    // zeroes the ones outside), each as 4-byte global_load_lds (LDS address =
+    // the wave-uniform base + 4 x lane).  Every wave stages exactly the bins and
+    // samples it loaded, after its own vmcnt(0): no cross-wave hand-off before
+    // the frame barrier.
+    constexpr int S4 = HOP / 4;  // clean samples per wave and frame
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    float* const rawN = (float*)(smem + W::OFF_RN);
+    const double* const rawC = (const double*)(smem + W::OFF_RC);
+    // One 4-byte LDS-DMA per lane, M0 = the wave-uniform LDS byte address.  As
+    // inline assembly: the compiler's wait pass treats a builtin LDS-DMA as a
+    // pending store to all of this one-array LDS and put a vmcnt(0) before the
+    // gain stage's first LDS read (draining the loads a frame early); the
+    // frame's only wait for them is the explicit vmcnt(0) before stage_rows.
+    // (Its own counted vmcnt waits stay correct beside these: they can only
+    // over-wait for loads issued after theirs.)
+    // (The base is made uniform inside the statement: in the out-of-line
+    // bodies of CSE_RUNWG_NOINLINE the compiler gave an "s" operand a VGPR.)
+    auto glds4 = [&](const float* src, unsigned char* dst) {
+        const unsigned m = (unsigned)(uintptr_t)(lds_ptr_t)dst;
+        int keep, base;
+        asm volatile("v_readfirstlane_b32 %1, %3\n\ts_nop 4\n\ts_mov_b32 %0, m0\n\t"
+                     "s_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                     "global_load_lds_dword %2, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep), "=&s"(base)
+                     : "v"(src), "v"(m)
+                     : "memory");
+    };
+    auto dma_rows = [&](int tt) {
+        if constexpr (W::DMA) {
+            if (tt < nf) {
+                const float* ys = (const float*)(Ybase + (int64_t)tt * B);
+                unsigned char* yb = smem + W::OFF_Y + (tt & 1) * W::YROW;
+                glds4(ys + 128 * wv + lane, yb + 512 * wv);
+                glds4(ys + 128 * wv + 64 + lane, yb + 512 * wv + 256);
+                if (wv == 0 && lane < 2) glds4(ys + 2 * M + lane, yb + 8 * M);  // bin M
+                if (nstride) {
+                    const float* ns = Nbase + (int64_t)tt * nstride;
+                    glds4(ns + 64 * wv + lane, (unsigned char*)rawN + 256 * wv);
+                    if (wv == 0 && lane == 0) glds4(ns + M, (unsigned char*)rawN + 4 * M);
+                }
+            }
+            if (cbase) {
 #pragma unroll
-        for (int u = 0; u < W::YPT; ++u) {
-            const int k = tid + u * W::THREADS;
-            if (k < B) pn[u] = Nbase[k];
+                for (int u = 0; u < 2 * S4 / 64; ++u) {
+                    const int d = 64 * u + lane;
+                    const int o = tt * HOP - NFFT / 2 + wv * S4 + (d >> 1) + lag;
+                    const int oc = o < 0 ? 0 : (o < len ? o : len - 1);
+                    glds4((const float*)(cbase + oc) + (d & 1),
+                          (unsigned char*)rawC + 8 * wv * S4 + 256 * u);
+                }
+            }
         }
+    };
+    // the derived rows of frame tt from the landed ones: thread tid stages bin
+    // tid (wave 0's thread 0 also bin M) and clean sample j = tid (tid < HOP
+    // ... as wave wv's lane < S4: j = wv S4 + lane).  Rows in buffer tt & 1:
+    // the G records (gamma_p, gamma_{M-p}, d_p, d_{M-p}) in pair order, d =
+    // max(gamma - 1, 0) or MMSE's (sqrt(pi)/2)/(gamma + 1e-12); SS: (N, P) and
+    // the unit phasor of Y written over Y; OMLSA's gamma times log2(e)
+    auto stage_rows = [&](int tt) {
+        if constexpr (W::DMA) {
+            if (tt < nf) {
+                float2* yrow = (float2*)(smem + W::OFF_Y + (tt & 1) * W::YROW);
+                float* grow = (float*)(smem + W::OFF_G + (tt & 1) * W::GROW);
+#pragma unroll
+                for (int u = 0; u < W::YPT; ++u) {
+                    const int k = tid + u * W::THREADS;
+                    if (k < B) {
+                        const float2 y = yrow[k];
+                        const float nv = rawN[k];
+                        const float P = y.x * y.x + y.y * y.y;
+                        const int pp = k <= M / 2 ? k : M - k, hh = k <= M / 2 ? 0 : 1;
+                        if (ALGO == CSE_ALGO_SS) {
+                            const float sc = fmaxf(fabsf(y.x), fabsf(y.y)) < 0x1p-50f ? 0x1p64f : 1.0f;
+                            const float yx = y.x * sc, yy = y.y * sc;
+                            const float pz = fmaf(yx, yx, yy * yy);
+                            const float r = __builtin_amdgcn_rsqf(pz);
+                            yrow[k] = pz > 0.0f ? make_float2(yx * r, yy * r)
+                                                : (pz == 0.0f ? make_float2(1.0f, 0.0f)
+                                                              : make_float2(pz - pz, pz - pz));
+                            grow[4 * pp + hh] = nv;
+                            grow[4 * pp + 2 + hh] = P;
+                        } else {
+                            const float gam = fmaxf(P * nv, EPS);
+                            grow[4 * pp + hh] = ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam;
+                            grow[4 * pp + 2 + hh] =
+                                ALGO == CSE_ALGO_MMSE ? 0.88622692545275801f * fast_rcp(gam + 1e-12f)
+                                                      : fmaxf(gam - 1.0f, 0.0f);
+                        }
+                    }
+                }
+            }
+            if (lane < S4) {
+                const int j = wv * S4 + lane;
+                const int o = tt * HOP - NFFT / 2 + j + lag;
+                const double v = (cbase && o >= 0 && o < len) ? rawC[j] : 0.0;
+                ((float*)(smem + W::OFF_C + (tt & 1) * W::HMAX * 4))[j] = (float)v;
+            }
+        }
+    };
+    if constexpr (W::DMA) {
+        if (!nstride) {  // a static noise row: loaded once
+            glds4(Nbase + 64 * wv + lane, (unsigned char*)rawN + 256 * wv);
+            if (wv == 0 && lane == 0) glds4(Nbase + M, (unsigned char*)rawN + 4 * M);
+        }
+        dma_rows(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stage_rows(0);
+    } else {
+        if (!nstride) {
+#pragma unroll
+            for (int u = 0; u < W::YPT; ++u) {
+                const int k = tid + u * W::THREADS;
+                if (k < B) pn[u] = Nbase[k];
+            }
+        }
+        load_rows(0);
+        store_rows(0);
+        load_rows(1);
     }
-    load_rows(0);
-    store_rows(0);
-    load_rows(1);
 
     const int b2 = (L == 16) ? i : (i & 15);
     const int h2 = (L == 16) ? 0 : (i >> 4);
-    const int off = 2 * b2 + 32 * h2;  // lane's first sample offset inside a frame
+    // lane's first sample offset inside a frame
+    const int off = W::SPLIT ? 2 * (i & 7) + 32 * (i >> 3) : 2 * b2 + 32 * h2;
 
     float rr[17];  // prev_gain**2 * prev_gamma per bin (read from frame 1 on)
 #pragma unroll
@@ -928,6 +1182,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         if (W::PK && t < nf) {
             // the frame in packed pairs (CSE_PK; same stages as the branch below)
             __syncthreads();
+            dma_rows(t + 1);  // W::DMA: frame t+1's rows, staged at the end of this frame
             CSE_MARK("gain");
             __builtin_amdgcn_s_setprio(1);
             f2 z[16];
@@ -936,7 +1191,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 const float alpha_t = (t == 0) ? 0.0f : cpar.p0;
                 const int yb = W::OFF_Y + (t & 1) * W::YROW, gb = W::OFF_G + (t & 1) * W::GROW;
                 const int ab = W::OFF_A + (t & 1) * W::AROW;
-                gain_pack_pk<NFFT, ALGO, OUT>((const float4*)(smem + yb), (const void*)(smem + gb),
+                gain_pack_pk<NFFT, ALGO, OUT, W::NAT>((const float4*)(smem + yb), (const void*)(smem + gb),
                                               (const float2*)(smem + ab), z, (f2*)(smem + creg + 72 * i),
                                               rr2, rrm, alpha_t, cpar,
                                               (const float4*)(smem + W::OFF_LC + W::ROTSTR * i),
@@ -991,7 +1246,68 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             }
             CSE_MARK("pass2");
             f2 v[16];
-            {
+            if constexpr (W::SPLIT) {
+                // x[b + 16 r'] = sum_i V[b][i] W16^{i r'} with i = c + 8 h:
+                //   even r' = 2s: DFT8_c of V[b][c] + V[b][c + 8]
+                //   odd r' = 2s + 1: DFT8_c of (V[b][c] - V[b][c + 8]) W16^c.
+                // Lane i = 8 hp + l reads columns 8 hp + c of row l (round 1) and
+                // of row l + 8 (round 2); u += sg dpp(u) with the partner lane
+                // i ^ 8 (row_ror:8 inside the cell's DPP row) gives hp = 0 the
+                // sums and hp = 1 the negated differences (the window entries of
+                // lanes hp = 1 are negated to match).
+                constexpr int TS2 = W::TS2;
+                const int l = i & 7, hp = i >> 3;
+                const float sg = hp ? -1.0f : 1.0f;
+                f2* blk_w = (f2*)(smem + creg) + i;                        // + TS2 b
+                const f2* blk_r = (const f2*)(smem + creg) + TS2 * l + 8 * hp;  // + c
+                auto radix2 = [&](f2 (&u)[8]) {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) {
+                        // v_mov_b32_dpp row_ror:8 (0x128): the value of lane i ^ 8
+                        auto ror8 = [](float x) {
+                            return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                0, __builtin_bit_cast(int, x), 0x128, 0xf, 0xf, false));
+                        };
+                        const f2 q = f2{ror8(u[c].x), ror8(u[c].y)};
+                        u[c] = pfma(q, pdup(sg), u[c]);
+                    }
+                };
+                f2 u0[8], u1[8];
+                wave_sync();
+#pragma unroll
+                for (int b = 0; b < 8; ++b) blk_w[TS2 * b] = z[b];
+                wave_sync();
+#pragma unroll
+                for (int c = 0; c < 8; ++c) u0[c] = blk_r[c];
+                wave_sync();  // round 1's reads are issued before round 2 overwrites
+#pragma unroll
+                for (int b = 0; b < 8; ++b) blk_w[TS2 * b] = z[8 + b];
+                radix2(u0);
+                wave_sync();
+#pragma unroll
+                for (int c = 0; c < 8; ++c) u1[c] = blk_r[c];
+                radix2(u1);
+                {  // the odd outputs' twiddles W16^c (lanes hp = 0: (1, 0))
+                    const float4* t4 = (const float4*)(smem + W::OFF_T2 + 80 * i);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const float4 q4 = t4[k];  // entries 2k, 2k + 1 (entry 0 unused)
+                        if (k > 0) {
+                            u0[2 * k] = p_cmul(u0[2 * k], f2{q4.x, q4.y});
+                            u1[2 * k] = p_cmul(u1[2 * k], f2{q4.x, q4.y});
+                        }
+                        u0[2 * k + 1] = p_cmul(u0[2 * k + 1], f2{q4.z, q4.w});
+                        u1[2 * k + 1] = p_cmul(u1[2 * k + 1], f2{q4.z, q4.w});
+                    }
+                }
+                idft8_pk(u0);
+                idft8_pk(u1);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    v[2 * q] = u0[q];
+                    v[2 * q + 1] = u1[q];
+                }
+            } else {
                 constexpr int TS = W::TS;
                 wave_sync();
                 f2* tw_ = (f2*)(smem + creg + 8 * i);
@@ -1014,8 +1330,8 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
 #pragma unroll
                     for (int r = 0; r < 16; ++r) v[r] = tr[r];
                 }
+                idft16_pk(v);
             }
-            idft16_pk(v);
             CSE_MARK("window");
 #pragma unroll
             for (int p = 0; p < 16; ++p) xp[p] = v[p];
@@ -1141,6 +1457,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             for (int q = 0; q < 32; ++q) x[q] = (q & 1) ? v[q >> 1].y : v[q >> 1].x;
         } else {
             __syncthreads();  // flush frames: clean row t visible, row t-1 reads done
+            dma_rows(t + 1);
             store_rows(t + 1);
             load_rows(t + 2);
 #pragma unroll
@@ -1168,6 +1485,9 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         float done[F];
         f2 done2[F / 2];
         if constexpr (W::PK) {  // slot pairs (q, q + 1) = (Re, Im) of one IFFT output
+            // (applying the window one ds_read_b128 at a time, fenced, to keep
+            // 4 of its 32 values live instead of 32: 13-pair A/B 26.3 against
+            // 22.8 ms, r05; the compiler's own schedule stays)
 #pragma unroll
             for (int p = 0; p < F / 2; ++p) {
                 done2[p] = pfma(xp[p], f2{win(2 * p), win(2 * p + 1)}, acc2[p]);
@@ -1206,14 +1526,15 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 // (one chain each: 24.51 -> two: 24.15 ms at 13 pairs)
                 float2 cl2[F / 2];  // the clean samples of slots q, q + 1
 #pragma unroll
-                for (int k = 0; k < F / 2; ++k) cl2[k] = *(const float2*)(crow_t + SP * k);
+                for (int k = 0; k < F / 2; ++k)
+                    cl2[k] = *(const float2*)(crow_t + slot_pos<W::SPLIT, SP>(2 * k));
                 float pa = 0.0f, pb = 0.0f, ca = 0.0f, cb = 0.0f;
                 if constexpr (W::PK) {  // the two chains as one pair
                     f2 pp = f2{0.0f, 0.0f}, cc = f2{0.0f, 0.0f};
 #pragma unroll
                     for (int p = 0; p < F / 2; ++p) {
                         const f2 y = done2[p];
-                        const int n = SP * p;
+                        const int n = slot_pos<W::SPLIT, SP>(2 * p);
                         if (head && yout && o0 + n < out_len) yout[o0 + n] = y.x;
                         if (head && yout && o0 + n + 1 < out_len) yout[o0 + n + 1] = y.y;
                         const f2 d = f2{cl2[p].x, cl2[p].y} - pmed3(y, -1.0f, 1.0f);
@@ -1227,7 +1548,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 }
 #pragma unroll
                 for (int q = 0; q < (W::PK ? 0 : F); ++q) {
-                    const int n = SP * (q >> 1) + (q & 1);
+                    const int n = slot_pos<W::SPLIT, SP>(q);
                     const float y = done[q];
                     if (head && yout && o0 + n < out_len) yout[o0 + n] = y;
                     // np.clip as one v_med3 (fminf(fmaxf()) of a value carried
@@ -1247,7 +1568,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
             } else {
 #pragma unroll
                 for (int q = 0; q < F; ++q) {
-                    const int n = SP * (q >> 1) + (q & 1);  // + off: position inside frame t
+                    const int n = slot_pos<W::SPLIT, SP>(q);  // + off: position inside frame t
                     const int o = o0 + n;
                     float iv = 1.0f;
                     if (edge) {
@@ -1277,6 +1598,10 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 }
             }
             sse += (double)part;
+        }
+        if constexpr (W::DMA) {  // this wave's loads of frame t+1 have landed: stage them
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            stage_rows(t + 1);
         }
         CSE_MARK("end");
     }
@@ -1313,20 +1638,26 @@ template <int NFFT, bool OUT>
 // 512 / CSE_WAVES_PER_SIMD VGPRs per lane
 __global__ void __launch_bounds__(WG<NFFT>::THREADS, CSE_WAVES_PER_SIMD)
     enhance_kernel(Args a) {
-    using W = WG<NFFT>;
+    using W = WG<NFFT, OUT>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wg = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t first = (int64_t)wg * W::CPWG;
     const int64_t left = a.n_cells - first;
     const int n = (int)(left < W::CPWG ? left : W::CPWG);
     const cse_cell_t* wcell = a.cells + first;
-    // hop and algorithm of the workgroup = its first cell's (host packs so);
-    // slots of another algorithm are skipped (finite never set).
+    // hop and algorithm of the workgroup = its first cell's (the host packs
+    // so); run_wg rejects slots that do not match them.  A group whose slot 0
+    // names no algorithm or an unsupported hop rejects every non-padding slot.
     const int hop = __builtin_amdgcn_readfirstlane(wcell[0].hop);
     const int algo = __builtin_amdgcn_readfirstlane(wcell[0].algo);
+    if ((hop != 128 && hop != 256) || algo < CSE_ALGO_SS || algo > CSE_ALGO_OMLSA) {
+        for (int c = threadIdx.x; c < n; c += W::THREADS)
+            if (wcell[c].algo != CSE_ALGO_NONE) reject_cell(a, first + c);
+        return;
+    }
     if (hop == 128)
         dispatch_algo<NFFT, 128, OUT>(a, wcell, n, algo, smem);
-    else if (hop == 256)
+    else
         dispatch_algo<NFFT, 256, OUT>(a, wcell, n, algo, smem);
 }
 
@@ -1389,11 +1720,11 @@ extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells
     int bytes, threads;
     if (n_fft == 512) {
         fn = enhance_fn_512(out);
-        bytes = WG<512>::BYTES;
+        bytes = out ? WG<512, true>::BYTES : WG<512, false>::BYTES;
         threads = WG<512>::THREADS;
     } else {
         fn = enhance_fn_1024(out);
-        bytes = WG<1024>::BYTES;
+        bytes = out ? WG<1024, true>::BYTES : WG<1024, false>::BYTES;
         threads = WG<1024>::THREADS;
     }
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) {

@@ -332,41 +332,55 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
     return red[0];
 }
 
-__global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs a) {
-    __shared__ cf buf[XHP];
-    __shared__ double red[XT];
-    __shared__ float rv[XT];
-    __shared__ int ri[XT];
-    __shared__ unsigned cbits[XWORDS];  // candidate lags k, bit k & 31 of word k >> 5
-    __shared__ int ncand;
-    const int cell = blockIdx.x, tid = threadIdx.x;
-    const int sig = a.sig_of[cell];
-    const float* e = a.head + a.head_offset[cell];
-    const int n = a.n, L = a.max_lag;
+// LDS of the lag kernel
+struct XcLds {
+    cf buf[XHP];
+    double red[XT];
+    float rv[XT];
+    int ri[XT];
+    unsigned cbits[XWORDS];  // candidate lags k, bit k & 31 of word k >> 5
+    int ncand;
+};
 
-    // C(f) = sum_b R_b(f) conj(S_b(f)).  Thread t owns the mirror pairs (f, XH - f),
-    // f = t + XT r, r < 8 (f = 0 pairs with the Nyquist bin XH), thread 0 also
-    // f = XH/2 (its own mirror): both bins of a pair come from the same two FFT
-    // points, X(f) = E + w O and X(XH - f) = conj(E - w O) (w = e^{-2πi f/XN}),
-    // so each point is read once, and the inverse transform's packing needs no
-    // exchange either.  The blocks tile e[0, n) exactly once, so the mean and
-    // energy of e are accumulated from the same loads (all 20 of a block's
-    // samples per lane are issued before the first is used: one memory latency
-    // per block, not 16).
-    cf C[8], Cm[8];  // C(f), C(XH - f)
-    cf Ch = cmk(0.0f, 0.0f);  // C(XH/2), thread 0
-#pragma unroll
-    for (int r = 0; r < 8; ++r) C[r] = Cm[r] = cmk(0.0f, 0.0f);
-    double s1 = 0.0, s2 = 0.0;
-    const float2* Rs = a.R + (int64_t)sig * a.nb * (XH + 1);
+struct XcPass {
+    double s1, s2;  // sum and energy of the head as fed (pass 1: centred)
+    int kmax;       // the fp32 argmax (ascending-lag first maximum)
+    int nc;         // lags within the margin, marked in cbits
+    int early;      // 0, or the status of a head whose correlation is the same at every lag
+};
+
+// One blocked-FFT correlation pass of one cell (see the file comment): head e,
+// its signal's clean spectra Rs, W(l) row Ws and ||r0||^2 rn; corr_row is the
+// cell's optional corr output row.
+// CENTRED = false: the raw head, mean corrected afterwards (c = c_raw - mu W),
+// fp32 error ~ ||r0|| ||e||.  CENTRED = true: the head minus its mean mu (as
+// two floats: (t - hi) - lo is within 2^-23 |t - mu| of the centred sample),
+// no correction, fp32 error ~ ||r0|| ||e - mu||.
+template <bool CENTRED>
+__device__ __forceinline__ void xcorr_pass(const float* e, const float2* Rs, const double* Ws,
+                                           double rn, int n, int L, int nb, float* corr_row,
+                                           XcLds& S, double mu, XcPass& o) {
+    cf* buf = S.buf;
+    double* red = S.red;
+    float* rv = S.rv;
+    int* ri = S.ri;
+    unsigned* cbits = S.cbits;
+    const int tid = threadIdx.x;
+    const float mu_hi = CENTRED ? (float)mu : 0.0f;
+    const float mu_lo = CENTRED ? (float)(mu - (double)mu_hi) : 0.0f;
     const cf rot_tid = bin_rotor(tid);
     const int pt = px(tid), mb = mirror_base(tid);
     // raw buffer over e[0, n) (CDNA buffer resource, word 3 = 0x00020000:
     // 32-bit data format, no swizzle); every offset issued lies inside it
     const __amdgpu_buffer_rsrc_t erc =
         __builtin_amdgcn_make_buffer_rsrc((void*)e, (short)0, 4 * n, 0x00020000);
+    cf C[8], Cm[8];  // C(f), C(XH - f)
+    cf Ch = cmk(0.0f, 0.0f);  // C(XH/2), thread 0
+#pragma unroll
+    for (int r = 0; r < 8; ++r) C[r] = Cm[r] = cmk(0.0f, 0.0f);
+    double s1 = 0.0, s2 = 0.0;
 #pragma unroll 1
-    for (int b = 0; b < a.nb; ++b) {
+    for (int b = 0; b < nb; ++b) {
         // samples v = 2 tid + (u & 1) + 512 (u >> 1) of the block; v < XB needs
         // u >> 1 <= 9 (and tid < 192 at 9).  In the last block the offsets are
         // clamped to the last sample and q >= n is masked to 0 here: the buffer
@@ -383,10 +397,11 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
                 const int qc = decltype(last)::value ? min(q, n - 1) : q;
                 const float t = __builtin_bit_cast(  // the builtin returns the raw 32 bits
                     float, __builtin_amdgcn_raw_buffer_load_b32(erc, 4 * qc, 0, 0));
-                x[u] = ((u < 18 || v < XB) && (!decltype(last)::value || q < n)) ? t : 0.0f;
+                const float tc = CENTRED ? (t - mu_hi) - mu_lo : t;
+                x[u] = ((u < 18 || v < XB) && (!decltype(last)::value || q < n)) ? tc : 0.0f;
             }
         };
-        if (b + 1 < a.nb)
+        if (b + 1 < nb)
             load_block(std::false_type());
         else
             load_block(std::true_type());
@@ -435,26 +450,20 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     }
     s1 = block_sum(s1, red);
     s2 = block_sum(s2, red);
-    if (!__builtin_isfinite(s1) || !__builtin_isfinite(s2)) {
-        if (tid == 0) {
-            a.lag[cell] = 0;
-            a.zero_energy[cell] = 0.0;
-            a.status[cell] = CSE_XCORR_NONFINITE;
-        }
+    o.s1 = s1;
+    o.s2 = s2;
+    o.early = 0;
+    if (!CENTRED && (!__builtin_isfinite(s1) || !__builtin_isfinite(s2) || !__builtin_isfinite(rn))) {
+        o.early = CSE_XCORR_NONFINITE;
         return;
     }
-    const double mu = s1 / n;
-    if (s2 == 0.0) {
-        // an all-zero head: sig0 = 0 exactly (its mean is 0), so scipy's
-        // correlation is 0 at every lag and np.argmax takes the first kept
-        // one, lag = -max_lag (no candidate re-evaluation: all 2 L + 1 tie)
-        if (tid == 0) {
-            a.lag[cell] = -L;
-            a.zero_energy[cell] = a.Z[(int64_t)sig * (2 * L + 1)];
-            a.status[cell] = CSE_XCORR_FLAT;
-        }
+    // an all-zero head (pass 0), a constant one (pass 1: the centred head is
+    // 0) or a constant clean head (r0 = 0): every c(l) is 0 exactly
+    if (s2 == 0.0 || rn == 0.0) {
+        o.early = CSE_XCORR_FLAT;
         return;
     }
+    const double mw = CENTRED ? 0.0 : s1 / n;  // the mean correction's weight
     // inverse real transform: Zi(f) = (C_f + conj C_{XH-f}) + i e^{+2πi f/XN} (C_f - conj C_{XH-f});
     // with ev, od those two terms, Zi(XH - f) = conj(ev - i t), t = e^{+2πi f/XN} od,
     // and Zi(XH/2) = 2 conj(C_{XH/2}): every point from the lane's own pairs
@@ -473,14 +482,13 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
     fft4096<1>(buf);
 
     // c(l) = c_raw(l) - mu W(l); c_raw[k] = (k even ? Re : Im) buf[k/2] / XN, k = l + L
-    const double* Ws = a.W + (int64_t)sig * (2 * L + 1);
     float best = -INFINITY;
     int bi = 0x7fffffff;
     for (int k = tid; k <= 2 * L; k += XT) {
         const cf z = buf[px(k >> 1)];
         const float craw = ((k & 1) ? z.y : z.x) * (1.0f / XN);
-        const float v = craw - (float)(mu * Ws[k]);
-        if (a.corr) a.corr[(int64_t)cell * (2 * L + 1) + k] = v;
+        const float v = craw - (float)(mw * Ws[k]);
+        if (corr_row) corr_row[k] = v;
         if (v > best) {  // k ascending per thread: first max kept
             best = v;
             bi = k;
@@ -501,27 +509,90 @@ __global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs 
         __syncthreads();
     }
     const float cmax = rv[0];
-    const int kmax = ri[0];
-    // the fp32 FFT works on the raw head (mean included: c = c_raw - mu W), so
-    // its error scales with ||r0|| ||e||, not ||r0|| ||e - mu||: a head with a
-    // large DC and little variance (a DC head: every true c(l) is 0) needs the
-    // raw energy s2 here, or fp32 noise picks the lag
-    const float delta = (float)(2e-5 * sqrt(a.rnorm[sig] * s2)) + 1e-30f;
-    if (tid == 0) ncand = 0;
+    o.kmax = ri[0];
+    // the fp32 FFT works on the head as it was fed (pass 0: the raw head, mean
+    // included: c = c_raw - mu W), so its error scales with ||r0|| ||fed||,
+    // not ||r0|| ||e - mu||: a head with a large DC and little variance (a DC
+    // head: every true c(l) is 0) needs the fed energy s2 here, or fp32 noise
+    // picks the lag
+    const float delta = (float)(2e-5 * sqrt(rn * s2)) + 1e-30f;
+    if (tid == 0) S.ncand = 0;
     for (int w = tid; w < XWORDS; w += XT) cbits[w] = 0u;
     __syncthreads();
     for (int k = tid; k <= 2 * L; k += XT) {
         const cf z = buf[px(k >> 1)];
-        const float v = ((k & 1) ? z.y : z.x) * (1.0f / XN) - (float)(mu * Ws[k]);
+        const float v = ((k & 1) ? z.y : z.x) * (1.0f / XN) - (float)(mw * Ws[k]);
         if (v >= cmax - delta) {
             atomicOr(&cbits[k >> 5], 1u << (k & 31));
-            atomicAdd(&ncand, 1);
+            atomicAdd(&S.ncand, 1);
         }
     }
     __syncthreads();
-    const int nc = ncand;
+    o.nc = S.ncand;
+}
+
+// the centred pass out of line: it runs only for flat cells, and inlined beside
+// pass 0 it cost the common path 30-40 spilled registers
+__device__ __noinline__ void xcorr_pass_centred(const float* e, const float2* Rs, const double* Ws,
+                                                double rn, int n, int L, int nb, float* corr_row,
+                                                XcLds& S, double mu, XcPass& o) {
+    xcorr_pass<true>(e, Rs, Ws, rn, n, L, nb, corr_row, S, mu, o);
+}
+
+__global__ void __launch_bounds__(XT, CSE_XC_WG_PER_CU) xcorr_lag_kernel(XcArgs a) {
+    __shared__ XcLds S;
+    cf* buf = S.buf;
+    double* red = S.red;
+    unsigned* cbits = S.cbits;
+    const int cell = blockIdx.x, tid = threadIdx.x;
+    const int sig = a.sig_of[cell];
+    const float* e = a.head + a.head_offset[cell];
+    const int n = a.n, L = a.max_lag;
+    // Pass 0 transforms the raw head (its mean is known only once every block
+    // is read).  When more than XCAND lags fall inside its margin (a head with
+    // a large mean and little else: a near-DC output, a flat correlation),
+    // pass 1 transforms the centred head e - mu, whose margin shrinks with the
+    // head's variance: the same lags, a handful of fp64 re-evaluations instead
+    // of one per lag (r04 re-evaluated up to 3,201 lags in fp64 serially in
+    // this workgroup: 43.6 ms for a DC-like head).
+    const float2* Rs = a.R + (int64_t)sig * a.nb * (XH + 1);
+    const double* Ws = a.W + (int64_t)sig * (2 * L + 1);
+    const double rn = a.rnorm[sig];
+    float* corr_row = a.corr ? a.corr + (int64_t)cell * (2 * L + 1) : nullptr;
+    XcPass o;
+    xcorr_pass<false>(e, Rs, Ws, rn, n, L, a.nb, corr_row, S, 0.0, o);
+    const double mu = o.s1 / n;
+    int status = CSE_XCORR_OK;
+    if (!o.early && o.nc > XCAND) {
+        status = CSE_XCORR_FLAT;
+        __syncthreads();  // every thread has read ncand and the buffer
+        xcorr_pass_centred(e, Rs, Ws, rn, n, L, a.nb, corr_row, S, mu, o);
+    }
+    if (o.early) {
+        // the correlation is the same at every lag, so np.argmax (:60) takes
+        // the first kept lag, -max_lag (max_lag < n: -max_lag is kept):
+        //  - NONFINITE: a NaN or inf in either head makes the mean-removed
+        //    head (:48-49) NaN (or -inf and NaN) everywhere, scipy's FFT
+        //    correlation NaN at every lag, and np.argmax of an all-NaN vector
+        //    0.  The cell is still shifted and length-matched; the finiteness
+        //    check comes after (:100-103), so a non-finite sample that the
+        //    shift drops does not skip the cell (the enhance kernel's lag-l
+        //    rescoring decides);
+        //  - FLAT: every c(l) is 0 (no candidate re-evaluation: all 2 L + 1 tie).
+        const bool nonfinite = o.early == CSE_XCORR_NONFINITE;
+        if (a.corr)
+            for (int k = tid; k <= 2 * L; k += XT)
+                a.corr[(int64_t)cell * (2 * L + 1) + k] = nonfinite ? __builtin_nanf("") : 0.0f;
+        if (tid == 0) {
+            a.lag[cell] = -L;
+            a.zero_energy[cell] = a.Z[(int64_t)sig * (2 * L + 1)];
+            a.status[cell] = o.early;
+        }
+        return;
+    }
+    const int nc = o.nc;
+    const int kmax = o.kmax;
     int kbest = kmax;
-    const int status = nc > XCAND ? CSE_XCORR_FLAT : CSE_XCORR_OK;
     if (nc > XCAND) {
         // a flat correlation (up to 2 L + 1 candidates): XG lags per pass over
         // the head, each thread's samples m = tid + XT i read once for all of

@@ -305,9 +305,10 @@ class GridPlan:
                 k = key_cache[ck] = (hop, noise_key(alg, p, n_frames(L, hop)))
                 keys.setdefault(k, None)
             item_key.append(k)
-        # jobs grouped by hop: each hop's rows are finished right after its own
-        # estimates (one cse_noise_finish launch per hop), so the first hop's
-        # finish can run while the next hop's chain does
+        # jobs grouped by hop: each hop's rows are finished by one
+        # cse_noise_finish launch right after that hop's own estimates (all on
+        # one stream, so in order; grouping by hop makes each launch's job list
+        # one contiguous slice)
         self.keys = sorted(keys, key=lambda k: k[0])
         self.pool_off, noff = {}, 0
         self.raw_off, roff = {}, 0
@@ -542,7 +543,9 @@ class GridPlan:
         if self.align:
             self.lag = self.lag_d.cpu().numpy()
             self.xstatus = self.xst_d.cpu().numpy()
-            fin &= self.xstatus != _lib.XCORR_NONFINITE
+            # a non-finite head aligns at -max_lag (np.argmax over an all-NaN
+            # correlation) and is rescored at that lag like any other: the
+            # reference checks finiteness only after the shift (:100-103)
             if self.rerun is not None:
                 sel, order, sse_r, fin_r = self.rerun
                 sr, fr = sse_r.cpu().numpy(), fin_r.cpu().numpy().astype(bool)

@@ -66,7 +66,8 @@ def alignment_lag(ref, sig, sr=16000, engine=None):
 def alignment_lag_status(ref, sig, sr=16000, engine=None):
     """(lag, cse_xcorr_lag status) — alignment_lag plus the status word
     (_lib.XCORR_OK, XCORR_FLAT: more than 64 near-maximal lags were
-    re-evaluated in fp64); (None, None) below 256 samples."""
+    re-evaluated in fp64, XCORR_NONFINITE: a NaN/inf in a head, lag -max_lag);
+    (None, None) below 256 samples."""
     import torch
     from .engine import Engine
     eng = engine or Engine()
@@ -91,8 +92,9 @@ def alignment_lag_status(ref, sig, sr=16000, engine=None):
                "cse_xcorr_prepare")
     _lib.check(lib.cse_xcorr_lag(_ptr(head), _ptr(off), _ptr(sig_of), 1, 1, n, max_lag, _ptr(ws),
                                  _ptr(lag), _ptr(zero), _ptr(status), None, st), "cse_xcorr_lag")
-    if int(status.item()) == _lib.XCORR_NONFINITE:
-        raise ValueError("alignment: non-finite samples in the signal")
+    # XCORR_NONFINITE: a NaN/inf in either head; the lag is -max_lag, the
+    # reference's np.argmax over its all-NaN correlation, and prepare_pair
+    # shifts by it like align_to_reference does (:60-69)
     return int(lag.item()), int(status.item())
 
 

@@ -57,10 +57,22 @@ TABLE_COLUMN = {"sse": 0, "snr": 1, "finite": 2, "stoi": 3, "lag": 4,
 NCOL = len(RECORD_FIELDS) - 1
 # bound on the cell waveforms held at once for STOI scoring (f32 bytes): 48 GiB
 # of the 288 GB HBM, i.e. 10 full 10-s pairs (7,308 computed cells x 640 KB each)
-# per batch, two batches in flight.  100-pair sweep (late r04, tools/call_r04s.sh):
+# per batch, two batches in flight.  100-pair sweep (late r04, call_r04s.sh in profiles/r04_commands.md):
 # 16 GiB 1.48-1.49 s, 32 GiB 1.31-1.32 s, 48 GiB 1.256-1.258 s, 64 GiB
 # 1.253-1.295 s; 96 GiB ran out of memory
 STOI_WAVE_BYTES = 48 << 30
+# share of the device memory free when a sweep starts that the two STOI
+# batches in flight may take together (a smaller GPU, or plans cached by the
+# caller, shrink the batches below STOI_WAVE_BYTES instead of running out)
+STOI_FREE_SHARE = 0.6
+
+
+def stoi_wave_bytes():
+    """Bytes of cell waveforms per STOI batch: STOI_WAVE_BYTES, capped at half
+    of STOI_FREE_SHARE of the device memory free now (two batches in flight)."""
+    import torch
+    free, _ = torch.cuda.mem_get_info()
+    return int(min(STOI_WAVE_BYTES, STOI_FREE_SHARE * free / 2))
 
 
 class JobSpecs(list):
@@ -258,7 +270,7 @@ def engine_compute(clean, noisy, specs, ids, engine=None, align=True, stoi=True)
 
     clean/noisy: lists of 1-D float arrays (host) indexed by pair.  Pairs are
     batched by length (the engine's signal batches are rectangular), and, when
-    STOI is scored, in groups whose cell waveforms fit STOI_WAVE_BYTES.  With
+    STOI is scored, in groups whose cell waveforms fit stoi_wave_bytes().  With
     job_specs' JobSpecs, cells the engine computes identically (a quarter of
     the HEAD grid: min_tracking ignores noise_percentile) are computed once
     and their rows copied, and batches of the same structure reuse one device
@@ -266,8 +278,9 @@ def engine_compute(clean, noisy, specs, ids, engine=None, align=True, stoi=True)
 
     Device memory: an engine made here is dropped with its cached plans on
     return.  A caller's engine keeps its plan_cache_size; the STOI path holds
-    two plans while it runs (double-buffered waveforms: 2 x STOI_WAVE_BYTES =
-    96 GiB peak plus each plan's analysis buffers) and trims the cache back to
+    two plans while it runs (double-buffered waveforms: 2 x stoi_wave_bytes(),
+    96 GiB peak on an idle 288-GB device, plus each plan's analysis buffers)
+    and trims the cache back to
     the caller's size on return."""
     from .engine import Engine
     own = engine is None
@@ -328,9 +341,10 @@ def _engine_compute(eng, clean, noisy, specs, ids, align, stoi):
         else:
             rows = {p: np.flatnonzero(pair_of == p) for p in pairs_l}
         batches, cur, n_cur = [], [], 0
+        cap = stoi_wave_bytes() if stoi else 0
         for pair in pairs_l:
             n = len(rows[pair])
-            if stoi and cur and (n_cur + n) * L * 4 > STOI_WAVE_BYTES:
+            if stoi and cur and (n_cur + n) * L * 4 > cap:
                 batches.append(cur)
                 cur, n_cur = [], 0
             cur.append(pair)
@@ -587,7 +601,7 @@ def optimize_parameters(clean_reference, noisy_audio, sr, algorithm, param_range
     optimize_parameters (speech_enhancement_comparison.py:109-252), scored by
     STOI and SNR: returns {'stoi': {'score', 'params', 'cell', 'snr'},
     'snr': {'score', 'params', 'cell', 'stoi'}, 'baseline': {'stoi', 'snr'},
-    'improvements': {'stoi', 'snr'}, 'table'}; raises ValueError like :251-253
+    'improvements': {'stoi', 'snr'}, 'table'}; raises ValueError like :233-235
     when no cell produced a finite output.  The 'stoi' entry is None when no
     cell has a STOI value (a compute function that does not score STOI)."""
     from .engine import canonical_algo
@@ -619,7 +633,7 @@ def optimize_parameters(clean_reference, noisy_audio, sr, algorithm, param_range
 
 def run_sweep(clean, noisy, stems, out_root, sr=16000, algorithms=None, grids=None,
               group=None, device=None):
-    """The reference's batch driver (main, speech_enhancement_comparison.py:378-474)
+    """The reference's batch driver (main, speech_enhancement_comparison.py:375-473)
     on the device: every pair x algorithm x grid cell scored after
     finalize_enhanced (STOI and SNR), the STOI-best and SNR-best cells per
     (pair, algorithm) selected by the sequential tolerance scan, their

@@ -65,7 +65,11 @@ enum {
  * of one such slot group (cells[g*G .. g*G+G-1]) MUST share algo, hop,
  * y_offset, noise_offset, noise_stride, clean_offset and lag; pad a short
  * group with CSE_ALGO_NONE slots.  Only param, out_offset and gain_offset may
- * differ.
+ * differ.  The kernel checks it: a non-padding slot whose shared fields differ
+ * from slot 0's is not computed and gets finite = 0, sse = NaN (the
+ * reference's skip, speech_enhancement_comparison.py:102-103; y_out / g_out
+ * untouched), and a group whose slot 0 is padding or names an unsupported
+ * algorithm or hop rejects every non-padding slot the same way.
  */
 typedef struct cse_cell {
     int32_t algo;          /* CSE_ALGO_* */
@@ -272,20 +276,28 @@ int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n
  * cse_xcorr_lag: per cell c, the cell's output samples y[0, n) at
  *   head + head_offset[c] (f32, e.g. written by cse_enhance_cells with
  *   out_len >= n), sig_of[c] = its signal.  Outputs:
- *     lag[c]          the alignment lag (0 when status is NONFINITE)
+ *     lag[c]          the alignment lag; -max_lag when status is NONFINITE (a NaN
+ *                     or inf in either head makes scipy's correlation NaN at
+ *                     every lag, and np.argmax of it is the first kept lag).
+ *                     The reference still shifts and length-matches such a
+ *                     cell and only then rejects it if a non-finite sample
+ *                     remains (:100-103): the lag-l sse/finite of
+ *                     cse_enhance_cells decide, as for any other lag
  *     zero_energy[c]  sum of clean^2 over the samples the shifted output leaves
  *                     as zero padding (l > 0: clean[0, l); l < 0: clean[len+l, len)),
  *                     to be added to the lag-l sse of cse_enhance_cells
  *     status[c]       CSE_XCORR_*
  *     corr            optional [n_cells][2 max_lag + 1] f32 c(l) (diagnostics), or NULL
- * Lags whose fp32 FFT correlation lies within 2e-5 ||r0|| ||s0|| of the maximum
+ * Lags whose fp32 FFT correlation lies within 2e-5 ||r0|| ||e|| of the maximum
+ * (e the raw head, mean included: the FFT sees it before the mean correction)
  * are re-evaluated exactly in fp64, every one of them: the lag is exact in both
- * OK and FLAT status (FLAT only reports that the slow path ran).
+ * OK and FLAT status (FLAT only reports that the slow path ran; an all-zero
+ * head is FLAT with lag -max_lag and corr rows of 0).
  */
 enum {
     CSE_XCORR_OK = 0,
     CSE_XCORR_FLAT = 1,      /* > 64 near-maximal lags (flat correlation), all re-evaluated in fp64 */
-    CSE_XCORR_NONFINITE = 2, /* non-finite output head: no alignment */
+    CSE_XCORR_NONFINITE = 2, /* non-finite head (output or clean): lag -max_lag, corr rows NaN */
 };
 int64_t cse_xcorr_workspace_bytes(int64_t n_sig, int64_t len, int n, int max_lag);
 int cse_xcorr_prepare(const double* clean, int64_t n_sig, int64_t len, int n, int max_lag,

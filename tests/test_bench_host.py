@@ -118,12 +118,14 @@ def test_job_units_match_shards():
 @pytest.mark.parametrize("n_fft", [512, 1024])
 def test_roofline_block_prices_the_committed_pmc(n_fft):
     """The line's VALU roofline from the committed PMC of this build
-    (profiles/pmc_enhance{n_fft}_r04.json, digest-matched): frac = the issue
-    cycles (VALU 2, transcendental 4 per wave64 instruction) / (1024 SIMDs x
-    2.4 GHz x kernel time), and frac_vs_dense_stream = the same instruction
-    counts at the rates tools/micro/valu_peak.hip measured (2.71 / 4.86
-    cycles) over the profiled clock.  No bandwidth is derived from SURVEY
-    8(d)'s nominal bytes."""
+    (profiles/pmc_enhance{n_fft}_r05.json, digest-matched), on the product
+    binary's own counts: frac = (2 x (VALU - TRANS) + 4 x TRANS) / (1024 SIMDs
+    x 2.4 GHz x kernel time) (a packed instruction counted once, at the scalar
+    rate); dense_at_occupancy = the same counts at the rates
+    tools/micro/valu_peak.hip measures at the kernel's waves per SIMD;
+    fp32_flops = SQ_INSTS_VALU_FLOPS_FP32 x 64 / time against 157.3 TF.  No
+    scalar-build pricing (r04's frac_vs_dense_stream) and no bandwidth derived
+    from SURVEY 8(d)'s nominal bytes."""
     import json
     units = 457237200
     pmc = bench.load_pmc(units, n_fft)
@@ -131,13 +133,21 @@ def test_roofline_block_prices_the_committed_pmc(n_fft):
         pytest.skip("no committed PMC profile of these kernel sources")
     ks_ms = pmc["kernel_ms"]
     r = bench.roofline_block(n_fft, units, ks_ms)
-    assert r["bound"] == "valu" and r["pmc_matches_build"]
+    assert r["bound"].startswith("valu") and r["pmc_matches_build"]
+    assert "frac_vs_dense_stream" not in r
     ks = ks_ms / 1e3
-    assert abs(r["frac"] - pmc["valu_issue_cycles"] / (bench.SIMDS * bench.CLOCK * ks)) < 1e-12
-    v, t = pmc["valu_insts_scalar_equiv"], pmc["trans_insts"]
-    dense = bench.DENSE_VALU_CYC * (v - t) + bench.DENSE_TRANS_CYC * t
-    assert abs(r["frac_vs_dense_stream"] - dense / (bench.SIMDS * pmc["clock_ghz_profiled"] * 1e9 * ks)) < 1e-12
-    # the committed profile: the datasheet fraction below 1, the dense-stream one near it
-    assert 0.5 < r["frac"] < 1.0 and 0.8 < r["frac_vs_dense_stream"] < 1.1
+    v, t = pmc["sq_insts_valu"], pmc["sq_insts_valu_trans"]
+    need = 2 * (v - t) + 4 * t
+    assert abs(r["frac"] - need / (bench.SIMDS * bench.CLOCK * ks)) < 1e-12
+    d = r.get("dense_at_occupancy")
+    if d:
+        fma, _, exp = bench.DENSE_CYC[pmc["waves_per_simd"]]
+        dense = fma * (v - t) + exp * t
+        assert abs(d["frac"] - dense / (bench.SIMDS * pmc["clock_ghz_profiled"] * 1e9 * ks)) < 1e-12
+    if pmc.get("sq_insts_valu_flops_fp32"):
+        f = r["fp32_flops"]
+        assert abs(f["frac"] - pmc["sq_insts_valu_flops_fp32"] * 64 / ks / 157.3e12) < 1e-12
+        assert 0 < f["frac"] < 1
+    assert 0.2 < r["frac"] < 1.0
     assert all("GBps" not in k or (r[k] or 0) < 8000 for k in r)
     json.dumps(r)  # the line must serialise

@@ -1,5 +1,5 @@
 // The VALU rate a SIMD actually sustains, in SHADER CYCLES (s_memtime,
-// converted with s_memrealtime's 100 MHz), at W = 1..8 waves per SIMD and C
+// converted with s_memrealtime's 100 MHz), at W = 1, 2, 3, 4, 6, 8 waves per SIMD and C
 // independent chains per lane: scalar v_fma_f32, packed v_pk_fma_f32 (two f32
 // operations), v_exp_f32, and the OMLSA bin's mix (27 f32 VALU + 6
 // transcendentals, tools' 2/4-cycle model: 66 cycles per bin).  The enhance
@@ -69,7 +69,8 @@ int main(int argc, char** argv) {
     // wave-instructions per item: 1, 1, 1, 33 (27 + 6)
     const double per_item[4] = {1, 1, 1, 33};
     printf("waves/SIMD | shader cycles per wave-instruction per SIMD (clock GHz): fma  pk_fma  exp  mix(33/item)\n");
-    for (int w = 1; w <= 8; w *= 2) {
+    const int ws[] = {1, 2, 3, 4, 6, 8};  // 3: the enhance kernel's own occupancy
+    for (int w : ws) {
         const int blocks = 256 * w;  // 4 waves per block, one per SIMD
         printf("%d |", w);
         for (int op = 0; op < 4; ++op) {

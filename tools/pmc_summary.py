@@ -28,6 +28,24 @@ KERNELS = {"enhance512": "enhance_kernel<512, false>", "enhance1024": "enhance_k
 SIMDS, VALU_CYC, TRANS_CYC = 1024, 2, 4  # transcendental = 2x v_fma_f32 (tools/micro/valu_rate.hip)
 
 
+def occupancy(trace, kname):
+    """(VGPRs, LDS bytes, waves per SIMD) of a kernel from a rocprofv3 kernel
+    trace: registers allocated in granules of 8 (512 per lane and SIMD), LDS
+    160 KiB per CU shared by workgroups of 4 waves (one per SIMD)."""
+    if not os.path.exists(trace):
+        return None
+    for r in csv.DictReader(open(trace)):
+        if kname in r["Kernel_Name"]:
+            v = int(r["VGPR_Count"]) + int(r.get("Accum_VGPR_Count") or 0)
+            lds = int(r["LDS_Block_Size"])
+            alloc = -(-v // 8) * 8
+            w = min(8, 512 // alloc)
+            if lds:
+                w = min(w, 163840 // lds)
+            return {"vgprs": v, "lds_bytes": lds, "waves_per_simd": w}
+    return None
+
+
 def stats(path):
     out = {}
     for r in csv.DictReader(open(path)):
@@ -110,29 +128,27 @@ def main(tag, rnd, units512=None, units1024=None):
         pmc, nd = counters(os.path.join(base, f"pmc_{pmcname}_*", "run_counter_collection.csv"), kname)
         summary["kernels"][key] = {"kernel": kname, "kernel_ms_rocprof": ms, "pmc_per_launch": pmc,
                                    "pmc_launches": nd, **derive(pmc, ms)}
-    # r04: the n_fft 512 kernel issues packed f32 (v_pk_*) instructions, two f32
-    # operations each, which SQ_INSTS_VALU counts once.  Its VALU issue cycles are
-    # therefore taken from the scalar build of the same sources (CSE_PK=0: every
-    # f32 operation its own instruction, pmc_s512_*), over the product build's
-    # own busy cycles; both builds' SQPK passes (pk512, s512_pk) are recorded.
+    # r05: the product binary's own counts are the basis (a packed v_pk_*
+    # instruction counted once: it issues at the scalar rate); the SQPK pass
+    # adds its FP32 FLOPs.  r04 priced the scalar build (CSE_PK=0) instead,
+    # which counts instructions the product does not issue; that build's passes
+    # are still summarised when present, as a record only.
+    for key, name, pk in (("enhance512", "512", "pk512"), ("enhance1024", "1024", "pk1024")):
+        k = summary["kernels"][key]
+        occ = occupancy(os.path.join(base, f"kt_{name}", "run_kernel_trace.csv"), KERNELS[key])
+        if occ:
+            k.update(occ)
+        ppk, _ = counters(os.path.join(base, f"pmc_{pk}", "run_counter_collection.csv"), KERNELS[key])
+        if ppk:
+            k["pmc_packed_counters_per_launch"] = ppk
+            k["flops_fp32"] = ppk.get("SQ_INSTS_VALU_FLOPS_FP32")
     k512 = summary["kernels"]["enhance512"]
     spmc, _ = counters(os.path.join(base, "pmc_s512_sq1", "run_counter_collection.csv"), KERNELS["enhance512"])
     spk, _ = counters(os.path.join(base, "pmc_s512_pk", "run_counter_collection.csv"), KERNELS["enhance512"])
     ppk, _ = counters(os.path.join(base, "pmc_pk512", "run_counter_collection.csv"), KERNELS["enhance512"])
-    if spmc:
+    if spmc:  # record only (see above)
         k512["pmc_scalar_build_per_launch"] = spmc
         k512["pmc_scalar_build_pk_pass_per_launch"] = spk
-        k512["pmc_packed_counters_per_launch"] = ppk
-        sd = derive(spmc, None)
-        busy = k512["pmc_per_launch"].get("SQ_BUSY_CYCLES")
-        if sd.get("valu_issue_cycles") and busy:
-            k512["valu_issue_cycles_own_count"] = k512.get("valu_issue_cycles")
-            k512["valu_issue_cycles"] = sd["valu_issue_cycles"]
-            k512["valu_frac"] = sd["valu_issue_cycles"] / (SIMDS * busy / 32)
-            k512["valu_issue_cycles_source"] = ("scalar build (CSE_PK=0) instruction counts: a packed f32 "
-                                                "instruction does the work of two scalar ones")
-            k512["valu_insts_scalar_equiv"] = spmc.get("SQ_INSTS_VALU")
-            k512["trans_insts"] = spmc.get("SQ_INSTS_VALU_TRANS_F32")
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
     json.dump(summary, open(os.path.join(REPO, "profiles", f"{rnd}_kernels.json"), "w"), indent=1)
     for key, units in (("enhance512", units512), ("enhance1024", units1024)):
@@ -146,12 +162,14 @@ def main(tag, rnd, units512=None, units1024=None):
                "sq_insts_valu": pmc.get("SQ_INSTS_VALU"), "sq_insts_valu_trans": pmc.get("SQ_INSTS_VALU_TRANS_F32"),
                "grbm_gui_active": pmc.get("GRBM_GUI_ACTIVE"),
                "sq_busy_cycles": pmc.get("SQ_BUSY_CYCLES"),
+               "sq_insts_valu_flops_fp32": k.get("flops_fp32"),
                "valu_frac": k.get("valu_frac"), "clock_ghz_profiled": k.get("clock_ghz_profiled"),
                "valu_issue_cycles": k.get("valu_issue_cycles"),
-               "valu_issue_cycles_source": k.get("valu_issue_cycles_source", "this build's counts"),
-               "valu_insts_scalar_equiv": k.get("valu_insts_scalar_equiv", pmc.get("SQ_INSTS_VALU")),
-               "trans_insts": k.get("trans_insts", pmc.get("SQ_INSTS_VALU_TRANS_F32")),
+               "valu_issue_cycles_source": "this build's own SQ_INSTS_VALU / _TRANS_F32 (packed counted once)",
+               "vgprs": k.get("vgprs"), "lds_bytes": k.get("lds_bytes"),
+               "waves_per_simd": k.get("waves_per_simd"),
                "share_wait_inst_any": k.get("share_wait_inst_any"),
+               "share_wait_any": k.get("share_wait_any"),
                "lds_conflict_cycles_per_lds_inst": k.get("lds_conflict_cycles_per_lds_inst"),
                "kernel_src_sha": src_sha,
                "source": f"profiles/{rnd}_kernels.json (tools/profile_all.sh {tag})"}

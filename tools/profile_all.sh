@@ -4,12 +4,12 @@
 #   enhance_kernel<512>  : bench.py (BASELINE config 4 job, 100 pairs) -- the bench line
 #   enhance_kernel<1024> : bench.py --nfft 1024
 #   stoi_cells_kernel, xcorr_*: tools/bench_sweep.py (full grid, 4 pairs)
-#     bash tools/profile_all.sh TAG [what...]     what in {kt512, kt1024, ktsweep, pmc512, pmc1024, pmcstoi, pmcpk, pmc512s}
+#     bash tools/profile_all.sh TAG [what...]     what in {kt512, kt1024, ktsweep, pmc512, pmc1024, pmcstoi, pmcpk, pmcpk1024, pmc512s}
 # Output under gpurun_out/prof_TAG/; tools/pmc_summary.py turns it into profiles/*.json.
 set -o pipefail
 TAG=${1:-dev}
 shift
-WHAT=${*:-kt512 kt1024 ktsweep pmc512 pmc1024 pmcstoi pmcpk pmc512s}
+WHAT=${*:-kt512 kt1024 ktsweep pmc512 pmc1024 pmcstoi pmcpk pmcpk1024}
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
@@ -50,6 +50,7 @@ for w in $WHAT; do
              pmc 1024_sq1 "$SQ1" $P1024 && pmc 1024_sq2 "$SQ2" $P1024 ;;
     pmcstoi) pmc stoi_f64 "$SQF64" $SWEEP && pmc stoi_sq2 "$SQ2" $SWEEP ;;
     pmcpk) pmc pk512 "$SQPK" $P512 ;;
+    pmcpk1024) pmc pk1024 "$SQPK" $P1024 ;;
     pmc512s) CSE_LIB=$SCALAR_LIB pmc s512_sq1 "$SQ1" $P512 && CSE_LIB=$SCALAR_LIB pmc s512_pk "$SQPK" $P512 ;;
     *) echo "unknown $w"; exit 1 ;;
   esac
