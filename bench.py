@@ -58,7 +58,8 @@ SIMDS = 1024                   # 256 CUs x 4 SIMD-32
 # what a dense, dependency-free VALU stream sustains per SIMD, in shader cycles
 # per wave-instruction (tools/micro/valu_peak.hip, profiles/r05_micro_valu_peak.txt),
 # by waves per SIMD: {waves: (v_fma_f32, v_pk_fma_f32, v_exp_f32)}
-DENSE_CYC = {3: (4.06, 3.94, 6.64), 4: (3.46, 3.31, 5.75), 8: (2.71, 2.64, 4.86)}
+DENSE_CYC = {1: (9.02, 7.52, 21.64), 2: (5.13, 4.70, 7.61), 3: (3.98, 3.76, 6.37),
+             4: (3.46, 3.31, 5.76), 6: (2.95, 2.86, 5.16), 8: (2.71, 2.64, 4.86)}
 FP32_PEAK = 157.3e12           # MI355X_MICROARCH.md: FP32 vector, spec
 VALU_CYC, TRANS_CYC = 2, 4     # wave64 issue cycles: v_fma_f32 (SIMD-32), transcendental (2x: tools/micro/valu_rate.hip)
 CLOCK = 2.4e9                  # max shader clock
@@ -641,6 +642,31 @@ def main():
         sys.exit("parity check failed: " + json.dumps(res["parity"]))
 
 
+def occupancy_probe():
+    """The r05 occupancy evidence (profiles/r05_occupancy_probe.json,
+    tools/occupancy_probe.sh): the r04 kernel reduced to OMLSA hop 128 with its
+    LDS cut to 35 KB (timing build, tools/probes/occupancy_probe4.patch) at 3
+    and at 4 waves/SIMD, and the full kernel with the split pass 2 (CSE_SPLIT_T)
+    at 3 and 4 (the 4-wave build spills 344 B/lane at 128 VGPRs)."""
+    path = os.path.join(REPO, "profiles", "r05_occupancy_probe.json")
+    if not os.path.exists(path):
+        return None
+    b = json.load(open(path))["builds"]
+    out = {"source": "profiles/r05_occupancy_probe.json"}
+    for k in ("p3", "p4", "s3", "s4", "libcse"):
+        if k in b:
+            e = b[k]
+            out[k] = {"kernel_ms": round(e["kernel_ms_median"], 3), "vgprs_alloc": e["vgprs_alloc"],
+                      "lds_bytes": e["lds_bytes"], "scratch_bytes_per_lane": e["scratch_bytes_per_lane"],
+                      "mean_waves_per_simd": round(e["mean_waves_per_simd"], 2),
+                      "share_wait_inst_any": round(e["share_wait_inst_any"], 3),
+                      "share_wait_any": round(e["share_wait_any"], 3),
+                      "share_active_inst_any": round(e["share_active_inst_any"], 3)}
+    if "p3" in b and "p4" in b:
+        out["p4_over_p3_time"] = b["p4"]["kernel_ms_median"] / b["p3"]["kernel_ms_median"]
+    return out
+
+
 def roofline_block(n_fft, units, kern_ms):
     """The enhance kernel against the resource it spends: VALU issue.
 
@@ -665,7 +691,8 @@ def roofline_block(n_fft, units, kern_ms):
     bytes_per_unit = 12 * (n_fft // 2 + 1)
     ks = kern_ms / 1e3
     nominal = units * bytes_per_unit
-    roof = {"bound": "valu issue (latency / occupancy-limited)", "achieved": None,
+    roof = {"bound": "issue (VALU + LDS) at 3 waves/SIMD; a 4th wave buys 3.9 % (occupancy_probe)",
+            "achieved": None,
             "peak": SIMDS * CLOCK / 1e9,
             "unit": "G SIMD issue-cycles/s (1024 SIMDs)", "frac": None, "traffic": None,
             "kernel": f"cse::enhance_kernel<{n_fft}>", "kernel_ms": kern_ms,
@@ -678,6 +705,8 @@ def roofline_block(n_fft, units, kern_ms):
             "pmc_traffic_over_nominal": None,
             "hbm_measured_GBps": None, "hbm_measured_frac": None,
             "kernel_src_sha": kernel_src_sha()}
+    if n_fft == 512:
+        roof["occupancy_probe"] = occupancy_probe()
     pmc = load_pmc(units, n_fft)
     if not pmc:
         roof["note"] = "no committed PMC profile for this launch size: VALU figures absent"

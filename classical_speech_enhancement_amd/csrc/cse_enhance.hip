@@ -37,17 +37,12 @@
 #ifndef CSE_ROT_TABLE_1024
 #define CSE_ROT_TABLE_1024 0  // 1024: packing rotors as base x W32^j (the table measured slower)
 #endif
+#ifndef CSE_T_ROWS
+#define CSE_T_ROWS 1  // n_fft 512 packed pass 2: lanes write block rows, read block columns
+#endif
 #ifndef CSE_SPLIT_T
 #define CSE_SPLIT_T 0  // n_fft 512 sweep kernel: pass 2 through a half block (see WG::SPLIT)
 #endif
-#ifndef CSE_NAT_Y
-#define CSE_NAT_Y 0
-#endif
-#ifndef CSE_DMA_ROWS
-#define CSE_DMA_ROWS 0  // n_fft 512 (packed, OUT = false): rows by LDS-DMA, staged at frame end
-#endif
-
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 namespace cse {
 
@@ -245,19 +240,6 @@ struct WG {
     static constexpr bool R2 = (NFFT == 512);
     // packed pairs (CSE_PK): the rows in mirror-pair order, 16-B records
     static constexpr bool PK = R2 ? CSE_PK : CSE_PK_1024;
-    // Rows by LDS-DMA (global_load_lds, no VGPR destination; the n_fft 512
-    // sweep kernel): every wave loads its quarter of frame t+1's Y row (natural
-    // bin order, the double-buffered row the gain stage reads), of the noise row
-    // and of the clean samples at the start of frame t, and stages its own
-    // quarter of the derived rows (gamma/d or gamma/cig records, the clean row)
-    // at the end of frame t, after its own vmcnt(0): the loads are in flight
-    // for a whole frame and hold no registers (r04 held 8 VGPRs of prefetched
-    // rows through every frame).  The OUT variant (gain matrices, tests) keeps
-    // register staging and the pair-order Y / A rows.
-    static constexpr bool DMA = R2 && PK && CSE_DMA_ROWS && !OUT;
-    // natural-order Y rows and MMSE's cig in the G record's d slot (DMA, or
-    // register staging with CSE_NAT_Y: experiments)
-    static constexpr bool NAT = DMA || (R2 && PK && CSE_NAT_Y && !OUT);
     // Pass 2 through half a transpose block (n_fft 512 sweep kernel): rows
     // b < 8 of the 16 x 16 block, then rows b >= 8, each lane reading half a
     // row; lanes i and i ^ 8 (one DPP row of the cell) finish the first
@@ -282,7 +264,7 @@ struct WG {
     static_assert(!SPLIT || (8 * TS2 * 8 <= XB && XB % 256 == 128), "half block in the exchange slots");
     static constexpr int YROW = ((G::B * 8 + 15) / 16) * 16;      // bytes of one Y row
     static constexpr int GROW = ((G::B * (R2 ? 8 : 4) + 15) / 16) * 16;
-    static constexpr int AROW = (R2 && !DMA) ? ((G::B * 4 + 15) / 16) * 16 : 0;
+    static constexpr int AROW = R2 ? ((G::B * 4 + 15) / 16) * 16 : 0;
     static constexpr int OFF_Y = CPWG * CREG;                     // float2[2][B] (double buffer)
     static constexpr int OFF_G = OFF_Y + 2 * YROW;
     static constexpr int OFF_A = OFF_G + 2 * GROW;
@@ -320,15 +302,10 @@ struct WG {
     static constexpr int WSLOTS = HALF_TABLES ? 16 : 32;
     static constexpr int WSTR = HALF_TABLES ? 20 : 36;
     static constexpr int OFF_WIN = OFF_CP + CPWG * 32;
-    // DMA: the landing rows of the noise (f32 [B]) and of the clean samples (f64 [HMAX]),
-    // each wave's quarter its own
-    static constexpr int OFF_RN = OFF_WIN + G::L * WSTR * 4;
-    static constexpr int RNB = DMA ? ((G::B * 4 + 15) / 16) * 16 : 0;
-    static constexpr int OFF_RC = OFF_RN + RNB;
     // SPLIT: the odd-output twiddles W16^c (c = 1..7) of lanes i >= 8, (1, 0)
     // for lanes i < 8 (branch-free, VGPR operands: as SGPR pairs of constants
     // the twiddles spilled 90 SGPRs), a row of 8 complex per lane, stride 80 B
-    static constexpr int OFF_T2 = OFF_RC + (DMA ? HMAX * 8 : 0);
+    static constexpr int OFF_T2 = OFF_WIN + G::L * WSTR * 4;
     static constexpr int BYTES = OFF_T2 + (SPLIT ? G::L * 80 : 0);
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
@@ -353,6 +330,13 @@ static_assert(WG<512>::CPWG == CSE_CELLS_PER_GROUP(512) &&
 // Ordering of LDS accesses between the lanes of ONE wave: the LDS executes a
 // wave's DS instructions in issue order, so a compiler-level barrier is all a
 // write->read or read->write hand-off inside the wave needs (no s_waitcnt).
+// an LDS byte offset the compiler cannot relate to others: two reads from
+// different opaque bases are never merged into one ds_read2 / wide read
+__device__ __forceinline__ int opaque_off(int off) {
+    asm volatile("" : "+v"(off));
+    return off;
+}
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -524,7 +508,7 @@ __device__ __forceinline__ f2 gain_pair(f2 gam, f2 d, f2 a, f2& rr, float alpha_
 // records (Y_p, Y_{M-p}) (16 B); at 512 (g_p, g_{M-p}, d_p, d_{M-p}) (16 B) and
 // MMSE's / SS's a pairs (8 B), at 1024 (g_p, g_{M-p}) (8 B).  Packing rotors:
 // the lane's table row (512) or base x W32^j (1024).
-template <int NFFT, int ALGO, bool OUT, bool NAT = false>
+template <int NFFT, int ALGO, bool OUT>
 __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
                                              const void* __restrict__ growv,
                                              const float2* __restrict__ a2row, f2 (&z)[16],
@@ -535,21 +519,8 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
                                              float* __restrict__ gout_row, int i) {
     constexpr int L = Geo<NFFT>::L, M = Geo<NFFT>::M;
     constexpr bool R2 = (NFFT == 512);
-    constexpr bool WANT_A = R2 && !NAT && (ALGO == CSE_ALGO_MMSE || (ALGO == CSE_ALGO_SS && OUT));
+    constexpr bool WANT_A = R2 && (ALGO == CSE_ALGO_MMSE || (ALGO == CSE_ALGO_SS && OUT));
     const float4* y4 = y4row + i;
-    // NAT (DMA rows): Y in natural bin order, bins k = i + L j and M - k read
-    // as two 8-byte records; the G record's d slot holds MMSE's
-    // (sqrt(pi)/2)/(gamma + 1e-12) and d = max(gamma - 1, 0) is formed here
-    const float2* ylo = (const float2*)y4row + i;
-    const float2* yhi = (const float2*)y4row + (M - i);
-    auto ldy = [&](int k) {  // the pair record of pair index k (NAT: two reads)
-        if constexpr (NAT) {
-            const float2 a = ylo[k], b = yhi[-k];
-            return make_float4(a.x, a.y, b.x, b.y);
-        } else {
-            return y4[k];
-        }
-    };
     const float4* g4 = (const float4*)growv + i;  // 512
     const float2* g2 = (const float2*)growv + i;  // 1024
     const float2* a2 = a2row + i;
@@ -559,15 +530,14 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
         const float2 v = g2[k];
         return make_float4(v.x, v.y, 0.0f, 0.0f);
     };
-    float4 yc = ldy(0), gc = ldg(0);
+    float4 yc = y4[0], gc = ldg(0);
     float2 ac = WANT_A ? a2[0] : make_float2(0.0f, 0.0f);
     const cf base = R2 ? cmk(1.0f, 0.0f) : *base_p;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         // next pair's rows (j = 7: bin M/2, the record of pair M/2)
         const int nx = (j < 7) ? L * (j + 1) : M / 2 - i;
-        const float4 yn = (NAT && j == 7) ? make_float4(ylo[nx].x, ylo[nx].y, 0.0f, 0.0f) : ldy(nx),
-                     gn = ldg(nx);
+        const float4 yn = y4[nx], gn = ldg(nx);
         const float2 an = WANT_A ? a2[nx] : make_float2(0.0f, 0.0f);
         f2 ya = f2{yc.x, yc.y}, yb = f2{yc.z, yc.w};
         f2 g;  // the pair's gains
@@ -582,15 +552,8 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
             ya = f2{y0.x, y0.y};  // 1024: the rescaled phasor source where Y is tiny
             yb = f2{y1.x, y1.y};
         } else {
-            if (NAT && ALGO == CSE_ALGO_MMSE) {  // record (gamma pair, cig pair)
-                const f2 gam = f2{gc.x, gc.y};
-                const f2 dm = gam - 1.0f;
-                g = gain_pair<NFFT, ALGO>(gam, f2{fmaxf(dm.x, 0.0f), fmaxf(dm.y, 0.0f)},
-                                          f2{gc.z, gc.w}, rr[j], alpha_t, cpar);
-            } else {
-                g = gain_pair<NFFT, ALGO>(f2{gc.x, gc.y}, f2{gc.z, gc.w}, f2{ac.x, ac.y}, rr[j],
-                                          alpha_t, cpar);
-            }
+            g = gain_pair<NFFT, ALGO>(f2{gc.x, gc.y}, f2{gc.z, gc.w}, f2{ac.x, ac.y}, rr[j],
+                                      alpha_t, cpar);
             s = g;
         }
         if (OUT && gout_row) {
@@ -622,9 +585,7 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
     // bin M/2: scalar, Z'[M/2] = 2 conj(X_{M/2})
     float2 ym = make_float2(yc.x, yc.y);
     float gm;
-    const RowV rvm = (NAT && ALGO == CSE_ALGO_MMSE) ? RowV{gc.x, fmaxf(gc.x - 1.0f, 0.0f), gc.z}
-                                                    : RowV{gc.x, gc.z, ac.x};
-    const float sm = 2.0f * gain_bin<NFFT, ALGO>(ym, rvm, rrm, alpha_t, cpar, gm);
+    const float sm = 2.0f * gain_bin<NFFT, ALGO>(ym, RowV{gc.x, gc.z, ac.x}, rrm, alpha_t, cpar, gm);
     if (OUT && gout_row && i == 0) gout_row[M / 2] = gm;
     xw[8] = f2{ym.x * sm, -ym.y * sm};
 }
@@ -922,7 +883,6 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
     // compiler wait (vmcnt(0)) for every row load right after issuing them
     double pc[W::CPT];
     auto load_rows = [&](int t) {  // issue loads of frame t's rows into registers
-        if constexpr (W::DMA) return;
         if (t < nf) {
 #pragma unroll
             for (int u = 0; u < W::YPT; ++u) {
@@ -946,7 +906,6 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
     // phasor of Y in place of Y and 1/|Y| (gain output) — computed once here
     // for the workgroup's cells instead of by each of them
     auto store_rows = [&](int t) {  // registers -> LDS rows of frame t
-        if constexpr (W::DMA) return;
         if (t < nf) {
             float2* yrow = (float2*)(smem + W::OFF_Y + (t & 1) * W::YROW);
             float* grow = (float*)(smem + W::OFF_G + (t & 1) * W::GROW);
@@ -963,9 +922,6 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                     const int pp = k <= M / 2 ? k : M - k, hh = k <= M / 2 ? 0 : 1;
                     auto put = [&](float2 yv, float gv, float dv) {
                         if constexpr (W::PK) {
-                            if constexpr (W::NAT)
-                                yrow[k] = yv;
-                            else
                                 yrow[2 * pp + hh] = yv;
                             grow[4 * pp + hh] = gv;
                             grow[4 * pp + 2 + hh] = dv;
@@ -999,8 +955,7 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                         const float gam = fmaxf(P * pn[u], EPS);
                         // OMLSA's bins take gamma log2(e) (gain_omlsa), d from gamma
                         put(y, ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam,
-                            (W::NAT && ALGO == CSE_ALGO_MMSE) ? 0.88622692545275801f * fast_rcp(gam + 1e-12f)
-                                                               : fmaxf(gam - 1.0f, 0.0f));
+                            fmaxf(gam - 1.0f, 0.0f));
                         if (ALGO == CSE_ALGO_MMSE)
                             arow[ai] = 0.88622692545275801f * fast_rcp(gam + 1e-12f);
                     }
@@ -1014,130 +969,16 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
             if (j < HOP) crow[j] = pc[u];
         }
     };
-    // ---- DMA rows (W::DMA): wave wv loads bins [64 wv, 64 wv + 64) of the Y row
-    // (into the double-buffered natural-order row the gain stage reads) and of
-    // the noise row, wave 0 also bin M, and the clean samples [wv S4, wv S4 +
-    // S4) (f64, as dword pairs; indices clamped into the signal, the stager
-    // zeroes the ones outside), each as 4-byte global_load_lds (LDS address =
-    // the wave-uniform base + 4 x lane).  Every wave stages exactly the bins and
-    // samples it loaded, after its own vmcnt(0): no cross-wave hand-off before
-    // the frame barrier.
-    constexpr int S4 = HOP / 4;  // clean samples per wave and frame
-    const int wv = __builtin_amdgcn_readfirstlane(wave);
-    float* const rawN = (float*)(smem + W::OFF_RN);
-    const double* const rawC = (const double*)(smem + W::OFF_RC);
-    // One 4-byte LDS-DMA per lane, M0 = the wave-uniform LDS byte address.  As
-    // inline assembly: the compiler's wait pass treats a builtin LDS-DMA as a
-    // pending store to all of this one-array LDS and put a vmcnt(0) before the
-    // gain stage's first LDS read (draining the loads a frame early); the
-    // frame's only wait for them is the explicit vmcnt(0) before stage_rows.
-    // (Its own counted vmcnt waits stay correct beside these: they can only
-    // over-wait for loads issued after theirs.)
-    // (The base is made uniform inside the statement: in the out-of-line
-    // bodies of CSE_RUNWG_NOINLINE the compiler gave an "s" operand a VGPR.)
-    auto glds4 = [&](const float* src, unsigned char* dst) {
-        const unsigned m = (unsigned)(uintptr_t)(lds_ptr_t)dst;
-        int keep, base;
-        asm volatile("v_readfirstlane_b32 %1, %3\n\ts_nop 4\n\ts_mov_b32 %0, m0\n\t"
-                     "s_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                     "global_load_lds_dword %2, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep), "=&s"(base)
-                     : "v"(src), "v"(m)
-                     : "memory");
-    };
-    auto dma_rows = [&](int tt) {
-        if constexpr (W::DMA) {
-            if (tt < nf) {
-                const float* ys = (const float*)(Ybase + (int64_t)tt * B);
-                unsigned char* yb = smem + W::OFF_Y + (tt & 1) * W::YROW;
-                glds4(ys + 128 * wv + lane, yb + 512 * wv);
-                glds4(ys + 128 * wv + 64 + lane, yb + 512 * wv + 256);
-                if (wv == 0 && lane < 2) glds4(ys + 2 * M + lane, yb + 8 * M);  // bin M
-                if (nstride) {
-                    const float* ns = Nbase + (int64_t)tt * nstride;
-                    glds4(ns + 64 * wv + lane, (unsigned char*)rawN + 256 * wv);
-                    if (wv == 0 && lane == 0) glds4(ns + M, (unsigned char*)rawN + 4 * M);
-                }
-            }
-            if (cbase) {
+    if (!nstride) {
 #pragma unroll
-                for (int u = 0; u < 2 * S4 / 64; ++u) {
-                    const int d = 64 * u + lane;
-                    const int o = tt * HOP - NFFT / 2 + wv * S4 + (d >> 1) + lag;
-                    const int oc = o < 0 ? 0 : (o < len ? o : len - 1);
-                    glds4((const float*)(cbase + oc) + (d & 1),
-                          (unsigned char*)rawC + 8 * wv * S4 + 256 * u);
-                }
-            }
+        for (int u = 0; u < W::YPT; ++u) {
+            const int k = tid + u * W::THREADS;
+            if (k < B) pn[u] = Nbase[k];
         }
-    };
-    // the derived rows of frame tt from the landed ones: thread tid stages bin
-    // tid (wave 0's thread 0 also bin M) and clean sample j = tid (tid < HOP
-    // ... as wave wv's lane < S4: j = wv S4 + lane).  Rows in buffer tt & 1:
-    // the G records (gamma_p, gamma_{M-p}, d_p, d_{M-p}) in pair order, d =
-    // max(gamma - 1, 0) or MMSE's (sqrt(pi)/2)/(gamma + 1e-12); SS: (N, P) and
-    // the unit phasor of Y written over Y; OMLSA's gamma times log2(e)
-    auto stage_rows = [&](int tt) {
-        if constexpr (W::DMA) {
-            if (tt < nf) {
-                float2* yrow = (float2*)(smem + W::OFF_Y + (tt & 1) * W::YROW);
-                float* grow = (float*)(smem + W::OFF_G + (tt & 1) * W::GROW);
-#pragma unroll
-                for (int u = 0; u < W::YPT; ++u) {
-                    const int k = tid + u * W::THREADS;
-                    if (k < B) {
-                        const float2 y = yrow[k];
-                        const float nv = rawN[k];
-                        const float P = y.x * y.x + y.y * y.y;
-                        const int pp = k <= M / 2 ? k : M - k, hh = k <= M / 2 ? 0 : 1;
-                        if (ALGO == CSE_ALGO_SS) {
-                            const float sc = fmaxf(fabsf(y.x), fabsf(y.y)) < 0x1p-50f ? 0x1p64f : 1.0f;
-                            const float yx = y.x * sc, yy = y.y * sc;
-                            const float pz = fmaf(yx, yx, yy * yy);
-                            const float r = __builtin_amdgcn_rsqf(pz);
-                            yrow[k] = pz > 0.0f ? make_float2(yx * r, yy * r)
-                                                : (pz == 0.0f ? make_float2(1.0f, 0.0f)
-                                                              : make_float2(pz - pz, pz - pz));
-                            grow[4 * pp + hh] = nv;
-                            grow[4 * pp + 2 + hh] = P;
-                        } else {
-                            const float gam = fmaxf(P * nv, EPS);
-                            grow[4 * pp + hh] = ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam;
-                            grow[4 * pp + 2 + hh] =
-                                ALGO == CSE_ALGO_MMSE ? 0.88622692545275801f * fast_rcp(gam + 1e-12f)
-                                                      : fmaxf(gam - 1.0f, 0.0f);
-                        }
-                    }
-                }
-            }
-            if (lane < S4) {
-                const int j = wv * S4 + lane;
-                const int o = tt * HOP - NFFT / 2 + j + lag;
-                const double v = (cbase && o >= 0 && o < len) ? rawC[j] : 0.0;
-                ((float*)(smem + W::OFF_C + (tt & 1) * W::HMAX * 4))[j] = (float)v;
-            }
-        }
-    };
-    if constexpr (W::DMA) {
-        if (!nstride) {  // a static noise row: loaded once
-            glds4(Nbase + 64 * wv + lane, (unsigned char*)rawN + 256 * wv);
-            if (wv == 0 && lane == 0) glds4(Nbase + M, (unsigned char*)rawN + 4 * M);
-        }
-        dma_rows(0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        stage_rows(0);
-    } else {
-        if (!nstride) {
-#pragma unroll
-            for (int u = 0; u < W::YPT; ++u) {
-                const int k = tid + u * W::THREADS;
-                if (k < B) pn[u] = Nbase[k];
-            }
-        }
-        load_rows(0);
-        store_rows(0);
-        load_rows(1);
     }
+    load_rows(0);
+    store_rows(0);
+    load_rows(1);
 
     const int b2 = (L == 16) ? i : (i & 15);
     const int h2 = (L == 16) ? 0 : (i >> 4);
@@ -1182,7 +1023,6 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
         if (W::PK && t < nf) {
             // the frame in packed pairs (CSE_PK; same stages as the branch below)
             __syncthreads();
-            dma_rows(t + 1);  // W::DMA: frame t+1's rows, staged at the end of this frame
             CSE_MARK("gain");
             __builtin_amdgcn_s_setprio(1);
             f2 z[16];
@@ -1191,7 +1031,7 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                 const float alpha_t = (t == 0) ? 0.0f : cpar.p0;
                 const int yb = W::OFF_Y + (t & 1) * W::YROW, gb = W::OFF_G + (t & 1) * W::GROW;
                 const int ab = W::OFF_A + (t & 1) * W::AROW;
-                gain_pack_pk<NFFT, ALGO, OUT, W::NAT>((const float4*)(smem + yb), (const void*)(smem + gb),
+                gain_pack_pk<NFFT, ALGO, OUT>((const float4*)(smem + yb), (const void*)(smem + gb),
                                               (const float2*)(smem + ab), z, (f2*)(smem + creg + 72 * i),
                                               rr2, rrm, alpha_t, cpar,
                                               (const float4*)(smem + W::OFF_LC + W::ROTSTR * i),
@@ -1203,9 +1043,19 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
             wave_sync();
             {
                 const int partner = (L - i) & (L - 1);
-                const f2* xr = (const f2*)(smem + creg + 72 * partner + (i == 0 ? 8 : 0));
+                const int xo = creg + 72 * partner + (i == 0 ? 8 : 0);
+                if constexpr (CSE_T_ROWS && L == 16) {
+                    // entries 7, 5, 3, 1 and 6, 4, 2, 0 from two unrelated bases:
+                    // 8 ds_read_b64 (2 LDS cycles each), not 4 ds_read2_b64 (8)
+                    const f2* xe = (const f2*)(smem + opaque_off(xo));
+                    const f2* xd = (const f2*)(smem + opaque_off(xo + 8));
 #pragma unroll
-                for (int s = 8; s < 16; ++s) z[s] = xr[15 - s];
+                    for (int s = 8; s < 16; ++s) z[s] = ((15 - s) & 1) ? xd[14 - s] : xe[15 - s];
+                } else {
+                    const f2* xr = (const f2*)(smem + xo);
+#pragma unroll
+                    for (int s = 8; s < 16; ++s) z[s] = xr[15 - s];
+                }
             }
             CSE_MARK("rows");
             store_rows(t + 1);
@@ -1310,6 +1160,24 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
             } else {
                 constexpr int TS = W::TS;
                 wave_sync();
+                if constexpr (CSE_T_ROWS && L == 16) {
+                    // lane i writes row i of the block (z[b] at column b), lane
+                    // b2 reads column b2: 16 ds_read_b64 at the row stride (the
+                    // row-wise read merged into 8 ds_read2_b64, 8 LDS cycles per
+                    // pair against 2 + 2); the even and odd columns' writes from
+                    // unrelated bases stay ds_write_b64
+                    f2* we = (f2*)(smem + opaque_off(creg + 8 * TS * i));
+                    f2* wd = (f2*)(smem + opaque_off(creg + 8 * TS * i + 8));
+#pragma unroll
+                    for (int b = 0; b < 16; b += 2) {
+                        we[b] = z[b];
+                        wd[b] = z[b + 1];
+                    }
+                    wave_sync();
+                    const f2* tc = (const f2*)(smem + creg + 8 * b2);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) v[r] = tc[r * TS];
+                } else {
                 f2* tw_ = (f2*)(smem + creg + 8 * i);
                 const f2* tr = (const f2*)(smem + creg + 8 * TS * b2);
 #pragma unroll
@@ -1329,6 +1197,7 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                 } else {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) v[r] = tr[r];
+                }
                 }
                 idft16_pk(v);
             }
@@ -1457,7 +1326,6 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
             for (int q = 0; q < 32; ++q) x[q] = (q & 1) ? v[q >> 1].y : v[q >> 1].x;
         } else {
             __syncthreads();  // flush frames: clean row t visible, row t-1 reads done
-            dma_rows(t + 1);
             store_rows(t + 1);
             load_rows(t + 2);
 #pragma unroll
@@ -1598,10 +1466,6 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                 }
             }
             sse += (double)part;
-        }
-        if constexpr (W::DMA) {  // this wave's loads of frame t+1 have landed: stage them
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            stage_rows(t + 1);
         }
         CSE_MARK("end");
     }
