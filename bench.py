@@ -691,7 +691,8 @@ def roofline_block(n_fft, units, kern_ms):
     bytes_per_unit = 12 * (n_fft // 2 + 1)
     ks = kern_ms / 1e3
     nominal = units * bytes_per_unit
-    roof = {"bound": "issue (VALU + LDS) at 3 waves/SIMD; a 4th wave buys 3.9 % (occupancy_probe)",
+    roof = {"bound": ("valu issue at the kernel's occupancy (3 waves/SIMD): see dense_at_occupancy, "
+                      "lds_array_busy and occupancy_probe (a 4th wave buys 3.9 %)"),
             "achieved": None,
             "peak": SIMDS * CLOCK / 1e9,
             "unit": "G SIMD issue-cycles/s (1024 SIMDs)", "frac": None, "traffic": None,
@@ -750,8 +751,8 @@ def roofline_block(n_fft, units, kern_ms):
                                   "frac": fl * 64 / ks / FP32_PEAK,
                                   "counter": ("SQ_INSTS_VALU_FLOPS_FP32 x 64: the counter counts per "
                                               "wave-instruction, weighted by FLOPs per lane")}
-        for k in ("share_wait_inst_any", "share_wait_any", "lds_conflict_cycles_per_lds_inst",
-                  "vgprs", "waves_per_simd"):
+        for k in ("share_wait_inst_any", "share_wait_any", "share_wait_inst_lds",
+                  "lds_array_busy", "lds_conflict_cycles_per_lds_inst", "vgprs", "waves_per_simd"):
             if pmc.get(k) is not None:
                 roof[k] = pmc[k]
     return roof

@@ -28,18 +28,23 @@ KERNELS = {"enhance512": "enhance_kernel<512, false>", "enhance1024": "enhance_k
 SIMDS, VALU_CYC, TRANS_CYC = 1024, 2, 4  # transcendental = 2x v_fma_f32 (tools/micro/valu_rate.hip)
 
 
+# WG<NFFT, false>::BYTES (dynamic LDS: the trace's LDS_Block_Size reads 0)
+LDS_BYTES = {"enhance_kernel<512, false>": 53600, "enhance_kernel<1024, false>": 52800}
+
+
 def occupancy(trace, kname):
-    """(VGPRs, LDS bytes, waves per SIMD) of a kernel from a rocprofv3 kernel
-    trace: registers allocated in granules of 8 (512 per lane and SIMD), LDS
-    160 KiB per CU shared by workgroups of 4 waves (one per SIMD)."""
+    """(VGPRs allocated, LDS bytes, waves per SIMD) of a kernel from a rocprofv3
+    kernel trace: this ROCm's trace gives VGPR_Count in units of 2 registers
+    (the 153-VGPR sweep kernel reads 80: 160 allocated, granule 8; 512 per lane
+    and SIMD), and the LDS of the dynamically sized kernels comes from
+    LDS_BYTES (160 KiB per CU shared by workgroups of 4 waves, one per SIMD)."""
     if not os.path.exists(trace):
         return None
     for r in csv.DictReader(open(trace)):
         if kname in r["Kernel_Name"]:
-            v = int(r["VGPR_Count"]) + int(r.get("Accum_VGPR_Count") or 0)
-            lds = int(r["LDS_Block_Size"])
-            alloc = -(-v // 8) * 8
-            w = min(8, 512 // alloc)
+            v = 2 * (int(r["VGPR_Count"]) + int(r.get("Accum_VGPR_Count") or 0))
+            lds = int(r["LDS_Block_Size"]) or LDS_BYTES.get(kname, 0)
+            w = min(8, 512 // v)
             if lds:
                 w = min(w, 163840 // lds)
             return {"vgprs": v, "lds_bytes": lds, "waves_per_simd": w}
@@ -96,6 +101,12 @@ def derive(pmc, kernel_ms):
                   "SQ_ACTIVE_INST_LDS"):
             if k in pmc:
                 d["share_" + k[3:].lower()] = pmc[k] / w
+    if "SQ_LDS_IDX_ACTIVE" in pmc and busy:
+        # LDS-array cycles (summed over the CUs) over the CU cycles of the launch
+        d["lds_array_busy"] = pmc["SQ_LDS_IDX_ACTIVE"] / (256 * busy / 32)
+        d["lds_cycles_per_lds_inst"] = pmc["SQ_LDS_IDX_ACTIVE"] / pmc["SQ_INSTS_LDS"]
+    if "SQ_WAIT_INST_LDS" in pmc and "SQ_WAVE_CYCLES" in pmc:
+        d["share_wait_inst_lds"] = pmc["SQ_WAIT_INST_LDS"] / pmc["SQ_WAVE_CYCLES"]
     if "SQ_LDS_BANK_CONFLICT" in pmc and "SQ_INSTS_LDS" in pmc:
         d["lds_conflict_cycles_per_lds_inst"] = pmc["SQ_LDS_BANK_CONFLICT"] / pmc["SQ_INSTS_LDS"]
     return d
@@ -171,6 +182,8 @@ def main(tag, rnd, units512=None, units1024=None):
                "share_wait_inst_any": k.get("share_wait_inst_any"),
                "share_wait_any": k.get("share_wait_any"),
                "lds_conflict_cycles_per_lds_inst": k.get("lds_conflict_cycles_per_lds_inst"),
+               "lds_array_busy": k.get("lds_array_busy"),
+               "share_wait_inst_lds": k.get("share_wait_inst_lds"),
                "kernel_src_sha": src_sha,
                "source": f"profiles/{rnd}_kernels.json (tools/profile_all.sh {tag})"}
         json.dump(out, open(os.path.join(REPO, "profiles", f"pmc_{key}_{rnd}.json"), "w"), indent=1)

@@ -4,7 +4,7 @@
 #   enhance_kernel<512>  : bench.py (BASELINE config 4 job, 100 pairs) -- the bench line
 #   enhance_kernel<1024> : bench.py --nfft 1024
 #   stoi_cells_kernel, xcorr_*: tools/bench_sweep.py (full grid, 4 pairs)
-#     bash tools/profile_all.sh TAG [what...]     what in {kt512, kt1024, ktsweep, pmc512, pmc1024, pmcstoi, pmcpk, pmcpk1024, pmc512s}
+#     bash tools/profile_all.sh TAG [what...]     what in {kt512, kt1024, ktsweep, pmc512, pmc1024, pmcstoi, pmcpk, pmcpk1024, pmclds, pmclds1024, pmc512s}
 # Output under gpurun_out/prof_TAG/; tools/pmc_summary.py turns it into profiles/*.json.
 set -o pipefail
 TAG=${1:-dev}
@@ -21,6 +21,9 @@ P1024="bench.py --nfft 1024 --steps 1 --warmup 0 --no-cpu-baseline --no-parity -
 SWEEP="tools/bench_sweep.py --pairs 4 --reps 1"
 SQ1="SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
 SQ2="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"
+# r05: LDS-array busy cycles and LDS-issue stalls (MI355X_MICROARCH.md: SQ_LDS_IDX_ACTIVE =
+# all LDS-array cycles, SQ_WAIT_INST_LDS = the LDS-issue share of SQ_WAIT_INST_ANY)
+SQLDS="SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
 SQF64="SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
 # r04: how the counters see packed f32 (v_pk_*) instructions
 SQPK="SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_FLOPS_FP32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
@@ -50,6 +53,8 @@ for w in $WHAT; do
              pmc 1024_sq1 "$SQ1" $P1024 && pmc 1024_sq2 "$SQ2" $P1024 ;;
     pmcstoi) pmc stoi_f64 "$SQF64" $SWEEP && pmc stoi_sq2 "$SQ2" $SWEEP ;;
     pmcpk) pmc pk512 "$SQPK" $P512 ;;
+    pmclds) pmc 512_lds "$SQLDS" $P512 ;;
+    pmclds1024) pmc 1024_lds "$SQLDS" $P1024 ;;
     pmcpk1024) pmc pk1024 "$SQPK" $P1024 ;;
     pmc512s) CSE_LIB=$SCALAR_LIB pmc s512_sq1 "$SQ1" $P512 && CSE_LIB=$SCALAR_LIB pmc s512_pk "$SQPK" $P512 ;;
     *) echo "unknown $w"; exit 1 ;;
