@@ -567,6 +567,7 @@ def main():
     # records gathered, both sequential selections
     sweep = None
     if not args.no_sweep:
+        torch.cuda.empty_cache()  # the timed jobs' plans are gone: their memory goes back
         sweep = sweep_block(args, world, total_pairs, weak)
 
     # ---- parity on every rank: the pair it holds most cells of, stratified
@@ -815,6 +816,7 @@ def sweep_block(args, world, total_pairs, weak):
            "xcorr_status": {"ok": int((st == 0).sum()), "flat": int((st == 1).sum()),
                             "nonfinite": int((st == 2).sum())},
            "nonzero_lags": int((table[:, 4] != 0).sum()),
+           "stoi_batch_wave_bytes": search.stoi_wave_bytes(),
            "winners": {"snr": sum(1 for v in best.values() if v[0] >= 0),
                        "stoi": sum(1 for v in best_stoi.values() if v[0] >= 0),
                        "groups": len(best)}}

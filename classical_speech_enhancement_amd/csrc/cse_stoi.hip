@@ -384,6 +384,31 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Per-stage timing (analysis builds only, -DCSE_STOI_STAMPS): shader-cycle
+// (s_memtime) deltas of the workgroup between its barriers, by stage, stored
+// per cell by thread 0 into the buffer cse_stoi_stamp_buffer() installs.
+//   0 tables + first block table   1 staging writes   2 resampling
+//   3 rfft (OLA/window, DFT16 x DFT16, transposes, |X|^2)   4 band sums
+//   5 phase B   6 whole kernel
+struct StoiStamps {
+#ifdef CSE_STOI_STAMPS
+    unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long last = 0, t0 = 0;
+    __device__ void start() { t0 = last = __builtin_amdgcn_s_memtime(); }
+    __device__ void mark(int k) {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        acc[k] += now - last;
+        last = now;
+    }
+#else
+    __device__ void start() {}
+    __device__ void mark(int) {}
+#endif
+};
+#ifdef CSE_STOI_STAMPS
+__device__ unsigned long long* g_stoi_stamps;
+#endif
+
 struct StoiLds {
     double wnd[stoi::FR];
     cd tw256[256];          // e^{-2πi k/256}
@@ -433,7 +458,7 @@ template <bool PRE>
 __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t len, int lag,
                              bool clip, const double* __restrict__ x10,
                              const double* __restrict__ coef, const int* __restrict__ btab,
-                             int nblk, double* __restrict__ env) {
+                             int nblk, double* __restrict__ env, StoiStamps& ts) {
     using namespace stoi;
     const int tid = threadIdx.x;
     // 16-kHz input samples of one staging chunk, loaded into registers one
@@ -476,6 +501,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
         __syncthreads();
         if (!PRE) fetch(L.tab[0], 0);
     }
+    ts.mark(0);
     for (int blk = 0; blk < nblk; ++blk) {
         const int* tb = L.tab[blk & 1];
         const int j0 = tb[T_J0], nf = tb[T_NF];
@@ -504,6 +530,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                     }
                 }
                 __syncthreads();  // stage (and the next block's table) visible
+                ts.mark(1);
                 if (c0 + NSL < D)
                     fetch(tb, c0 + NSL);
                 else if (blk + 1 < nblk)
@@ -569,6 +596,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                     }
                 }
                 __syncthreads();  // e10 complete (also ends the chunk loop's last pass)
+                ts.mark(2);
             }
         }
         if (PRE) __syncthreads();
@@ -641,11 +669,25 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
             // ---- band envelopes of the frame by its own 16 lanes (one wave:
             // no workgroup barrier; the next block's first barrier protects pw)
             wave_sync();
+            ts.mark(3);
             if (n1 < NBAND && fl < nf) {
-                double s = 0.0;
-                for (int k = BAND_EDGE[n1]; k < BAND_EDGE[n1 + 1]; ++k) s += pw[k];
+                // 8 reads in flight per round into 4 partial sums: the serial
+                // read-and-add over the top band (45 bins) was 12 % of the
+                // kernel (tools/stoi_stages.py); the oracle's band sum is a
+                // matrix product, its order unspecified
+                const int k0 = BAND_EDGE[n1], k1e = BAND_EDGE[n1 + 1];
+                double s4[4] = {0.0, 0.0, 0.0, 0.0};
+                for (int k = k0; k < k1e; k += 8) {
+                    double q[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) q[u] = (k + u < k1e) ? pw[k + u] : 0.0;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) s4[u & 3] += q[u];
+                }
+                const double s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
                 env[(int64_t)(j0 + fl) * 16 + n1] = 0.5 * sqrt(s);
             }
+            ts.mark(4);
         }
     }
 }
@@ -661,8 +703,9 @@ __global__ void __launch_bounds__(stoi::NT) stoi_clean_env_kernel(const double* 
     const int sig = blockIdx.x;
     stoi_tables(L);
     const int nblk = meta[stoi::META * sig + 4];
+    StoiStamps ts;
     stoi_phase_a<true>(L, nullptr, 0, 0, false, x10all + (int64_t)sig * n10, nullptr,
-                       btab + (int64_t)sig * NBLK * stoi::BT, nblk, xtob + (int64_t)sig * Mmax * 16);
+                       btab + (int64_t)sig * NBLK * stoi::BT, nblk, xtob + (int64_t)sig * Mmax * 16, ts);
 }
 
 // (||x||, mean, 1/(||x - mean|| + eps)) of the clean envelope over each segment
@@ -730,12 +773,15 @@ __global__ void __launch_bounds__(stoi::NT, 3) stoi_cells_kernel(StoiArgs a,
         if (tid == 0) a.out[c] = 1e-5;
         return;
     }
+    StoiStamps ts;
+    ts.start();
     stoi_tables(L);
     double* env = a.scratch + c * a.Mmax * 16;
     const int lag = a.lag ? a.lag[c] : 0;
     stoi_phase_a<false>(L, a.y + a.y_offset[c], a.len, lag, a.clip != 0, nullptr, coef,
-                        a.btab + (int64_t)sig * a.NBLK * BT, a.meta[META * sig + 4], env);
+                        a.btab + (int64_t)sig * a.NBLK * BT, a.meta[META * sig + 4], env, ts);
     __syncthreads();  // env rows of this workgroup are visible to it
+    ts.mark(4);
     // ---- phase B: segment j, band b
     const double* xt = a.xtob + (int64_t)sig * a.Mmax * 16;
     const double4* xs = a.xstat + (int64_t)sig * a.Jmax * 16;
@@ -807,6 +853,14 @@ __global__ void __launch_bounds__(stoi::NT, 3) stoi_cells_kernel(StoiArgs a,
         for (int w = 0; w < NT / 64; ++w) s += L.red[w];
         a.out[c] = s / ((double)J * NBAND);
     }
+#ifdef CSE_STOI_STAMPS
+    ts.mark(5);
+    if (tid == 0 && g_stoi_stamps) {
+        ts.acc[6] = ts.last - ts.t0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g_stoi_stamps[c * 8 + k] = ts.acc[k];
+    }
+#endif
 }
 
 }  // namespace cse
@@ -858,6 +912,15 @@ extern "C" int cse_stoi_prepare(const double* clean, int64_t n_sig, int64_t len,
     CSE_CHECK_LAUNCH("cse_stoi_prepare");
     return CSE_OK;
 }
+
+#ifdef CSE_STOI_STAMPS
+// analysis builds only: per-cell stage cycles into buf [n_cells][8] (u64), or off (NULL)
+extern "C" int cse_stoi_stamp_buffer(void* buf) {
+    unsigned long long* p = (unsigned long long*)buf;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stoi_stamps), &p, sizeof(p)) == hipSuccess ? CSE_OK
+                                                                                        : CSE_ELAUNCH;
+}
+#endif
 
 extern "C" int cse_stoi_cells(const float* y, const int64_t* y_offset, const int32_t* lag,
                               const int32_t* sig_of, int64_t n_cells, int64_t n_sig, int64_t len,

@@ -72,6 +72,9 @@ def stoi_wave_bytes():
     of STOI_FREE_SHARE of the device memory free now (two batches in flight)."""
     import torch
     free, _ = torch.cuda.mem_get_info()
+    # blocks torch's caching allocator holds but no tensor uses are free to this
+    # process too (mem_get_info counts them as taken)
+    free += torch.cuda.memory_reserved() - torch.cuda.memory_allocated()
     return int(min(STOI_WAVE_BYTES, STOI_FREE_SHARE * free / 2))
 
 
