@@ -49,7 +49,7 @@ assert ctypes.sizeof(NoiseParams) == 48
 EXPORTS = ("cse_version", "cse_last_error", "cse_cells_per_group", "cse_stft",
            "cse_noise_workspace_bytes", "cse_noise_default_params", "cse_noise_estimate_ex",
            "cse_noise_estimate", "cse_noise_smooth", "cse_noise_median",
-           "cse_noise_percentile_med", "cse_noise_percentile_med2", "cse_noise_min_tracking_med", "cse_noise_finish",
+           "cse_noise_percentile_med", "cse_noise_percentile_med2", "cse_noise_percentile_quad", "cse_noise_min_tracking_med", "cse_noise_finish",
            "cse_noise_invert", "cse_istft_norm", "cse_enhance_cells",
            "cse_xcorr_workspace_bytes", "cse_xcorr_prepare", "cse_xcorr_lag",
            "cse_stoi_workspace_bytes", "cse_stoi_scratch_bytes", "cse_stoi_prepare",
@@ -106,6 +106,9 @@ def load(path=LIB_PATH):
     lib.cse_noise_percentile_med.argtypes = [P, P, i64, i32, i32, f64, f64, P, P, P]
     lib.cse_noise_percentile_med2.restype = i32
     lib.cse_noise_percentile_med2.argtypes = [P, P, i64, i32, i32, f64, f64, f64, P, P, P, P]
+    lib.cse_noise_percentile_quad.restype = i32
+    lib.cse_noise_percentile_quad.argtypes = [P, P, i64, i32, i32, f64, f64, f64, f64, P, P, P, P, P,
+                                              P]
     lib.cse_noise_min_tracking_med.restype = i32
     lib.cse_noise_min_tracking_med.argtypes = [P, P, i64, i32, i32, f64, P, f64, P, P, P]
     lib.cse_noise_finish.restype = i32

@@ -111,24 +111,48 @@ __global__ void __launch_bounds__(256) frame_energy_kernel(const double* __restr
     if (lane == 0) energy[sig * T + t] = s / (double)B;
 }
 
+// the same for two eps values from one read of P: the logs differ only where
+// P is below the larger eps (bit-identical to two frame_energy_kernel passes:
+// same operands, same order)
+__global__ void __launch_bounds__(256) frame_energy2_kernel(const double* __restrict__ P, int T,
+                                                            int B, double eps0, double eps1,
+                                                            double* __restrict__ energy0,
+                                                            double* __restrict__ energy1) {
+    const int lane = threadIdx.x & 63;
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t sig = blockIdx.y;
+    if (t >= T) return;
+    const double* row = P + (sig * T + t) * (int64_t)B;
+    const double hi = fmax(eps0, eps1);
+    double s0 = 0.0, s1 = 0.0;
+    for (int b = lane; b < B; b += 64) {
+        const double x = row[b];
+        const double l0 = log(fmax(x, eps0));
+        s0 += l0;
+        s1 += x >= hi ? l0 : log(fmax(x, eps1));
+    }
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+        s0 += __shfl_xor(s0, m, 64);
+        s1 += __shfl_xor(s1, m, 64);
+    }
+    if (lane == 0) {
+        energy0[sig * T + t] = s0 / (double)B;
+        energy1[sig * T + t] = s1 / (double)B;
+    }
+}
+
 // k quietest frames: argsort(energy)[:k], ties by frame index.  Only the
 // energies are sorted (8 B per frame of LDS, so T <= kMaxSortFrames fits);
 // the index set is then recovered exactly: every frame below the k-th
 // smallest energy thr, plus the lowest-index frames equal to thr.  The output
 // order is frame order (the percentile that consumes it sorts the values).
-__global__ void select_quiet_kernel(const double* __restrict__ energy, int T, int n2, int k,
-                                    int* __restrict__ sel) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double* key = (double*)smem;
-    const int64_t sig = blockIdx.x;
-    const double* e = energy + sig * T;
-    for (int i = threadIdx.x; i < n2; i += blockDim.x) key[i] = i < T ? e[i] : INFINITY;
-    __syncthreads();
-    bitonic_sort(key, nullptr, n2);
+// The selection of the k quietest frames given the sorted energies key[].
+__device__ void select_from_sorted(const double* __restrict__ e, const double* key, int* scan,
+                                   int T, int k, int* __restrict__ sel) {
     const double thr = key[k - 1];
     // each thread a contiguous chunk of frames; two block scans give every
     // thread its share of the ties (lowest index first) and its output slot
-    int* scan = (int*)(key + n2);  // blockDim.x ints after the sort buffer
     const int tid = threadIdx.x, nt = blockDim.x;
     const int chunk = (T + nt - 1) / nt;
     const int i0 = min(T, tid * chunk), i1 = min(T, i0 + chunk);
@@ -160,8 +184,26 @@ __global__ void select_quiet_kernel(const double* __restrict__ energy, int T, in
     int out = outs.x, taken = 0;
     for (int i = i0; i < i1; ++i) {
         const double v = e[i];
-        if (v < thr || (v == thr && taken++ < take_eq)) sel[sig * (int64_t)T + out++] = i;
+        if (v < thr || (v == thr && taken++ < take_eq)) sel[out++] = i;
     }
+}
+
+// grid (n_sig, sets): energy set y = energy + y n_sig T; one sort of the
+// signal's energies serves k0 (-> sel0) and, if sel1, k1 (-> sel1), each set's
+// outputs at + y n_sig T
+__global__ void select_quiet_kernel(const double* __restrict__ energy, int T, int n2, int k0,
+                                    int* __restrict__ sel0, int k1, int* __restrict__ sel1) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double* key = (double*)smem;
+    const int64_t sig = blockIdx.x;
+    const int64_t set = (int64_t)blockIdx.y * gridDim.x * T;
+    const double* e = energy + set + sig * T;
+    for (int i = threadIdx.x; i < n2; i += blockDim.x) key[i] = i < T ? e[i] : INFINITY;
+    __syncthreads();
+    bitonic_sort(key, nullptr, n2);
+    int* scan = (int*)(key + n2);  // blockDim.x ints after the sort buffer
+    select_from_sorted(e, key, scan, T, k0, sel0 + set + sig * T);
+    if (sel1) select_from_sorted(e, key, scan, T, k1, sel1 + set + sig * T);
 }
 
 enum { STATS_MEDIAN = 0, STATS_PERCENTILE = 1, STATS_SIMPLE = 2 };
@@ -227,7 +269,14 @@ __device__ __forceinline__ double wave_at(const double (&v)[E], int lane, int id
 template <int E>
 __global__ void __launch_bounds__(256) bin_stats_wave_kernel(
     const double* __restrict__ P, int T, int B, int mode, const int* __restrict__ sel, int k,
-    double q, double floor_rel, double eps, double* __restrict__ med, float* __restrict__ N) {
+    double q, double floor_rel, double eps, double* __restrict__ med, float* __restrict__ N,
+    const int* __restrict__ sel_z1, double eps_z1, float* __restrict__ N_z1) {
+    if (blockIdx.z == 1) {  // the second estimate of a two-estimate launch
+        sel = sel_z1;
+        eps = eps_z1;
+        N = N_z1;
+    }
+    if (mode != STATS_MEDIAN && !N) return;
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t sig = blockIdx.y;
@@ -257,27 +306,35 @@ __global__ void __launch_bounds__(256) bin_stats_wave_kernel(
     if (lane == 0) N[sig * B + b] = (float)fmax(est, eps);
 }
 
+// the second estimate (z1): a launch with grid z = 2 when sel_z1 is given
+struct StatsZ1 {
+    const int* sel = nullptr;
+    double eps = 0.0;
+    float* N = nullptr;
+};
+
 template <int E>
 static void launch_stats_wave(const double* P, int64_t n_sig, int T, int B, int mode,
                               const int* sel, int k, double q, double floor_rel, double eps,
-                              double* med, float* N, hipStream_t s) {
-    hipLaunchKernelGGL(bin_stats_wave_kernel<E>, dim3((B + 3) / 4, (unsigned)n_sig), dim3(256), 0,
-                       s, P, T, B, mode, sel, k, q, floor_rel, eps, med, N);
+                              double* med, float* N, StatsZ1 z1, hipStream_t s) {
+    hipLaunchKernelGGL(bin_stats_wave_kernel<E>,
+                       dim3((B + 3) / 4, (unsigned)n_sig, z1.sel ? 2u : 1u), dim3(256), 0,
+                       s, P, T, B, mode, sel, k, q, floor_rel, eps, med, N, z1.sel, z1.eps, z1.N);
 }
 
 // the wave path for n <= 2048 sort slots; false: use the LDS path
 static bool stats_wave(int n, const double* P, int64_t n_sig, int T, int B, int mode,
                        const int* sel, int k, double q, double floor_rel, double eps, double* med,
-                       float* N, hipStream_t s) {
+                       float* N, hipStream_t s, StatsZ1 z1 = StatsZ1()) {
     if (n > 2048 || n < 1) return false;
     const int n2 = n <= 64 ? 64 : next_pow2(n);
     switch (n2 / 64) {
-        case 1: launch_stats_wave<1>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, s); break;
-        case 2: launch_stats_wave<2>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, s); break;
-        case 4: launch_stats_wave<4>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, s); break;
-        case 8: launch_stats_wave<8>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, s); break;
-        case 16: launch_stats_wave<16>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, s); break;
-        default: launch_stats_wave<32>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, s); break;
+        case 1: launch_stats_wave<1>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, z1, s); break;
+        case 2: launch_stats_wave<2>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, z1, s); break;
+        case 4: launch_stats_wave<4>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, z1, s); break;
+        case 8: launch_stats_wave<8>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, z1, s); break;
+        case 16: launch_stats_wave<16>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, z1, s); break;
+        default: launch_stats_wave<32>(P, n_sig, T, B, mode, sel, k, q, floor_rel, eps, med, N, z1, s); break;
     }
     return true;
 }
@@ -503,63 +560,65 @@ __global__ void invert_kernel(const float* __restrict__ N, int64_t n, double eps
 // frames, one block ahead, with no per-frame conditions: r03's form (a bounds
 // check per load and per store) compiled to a branch per access and a full
 // vmcnt(0) wait per block.
-template <bool INV>
-__device__ __forceinline__ void finish_row(const float* __restrict__ Ns, float* __restrict__ Os,
-                                           int B, int nsrc, int nfr, double mu, float ief) {
-    const double c = 1.0 - mu;
-    // 1/max(v, eps) in fp32 (correctly rounded 1/x of the rounded operand:
-    // within 1.5 ulp of the fp64 quotient, which the f32 row stores anyway);
-    // the fp64 divide made this launch latency-bound
-    auto out = [&](double v) { return INV ? 1.0f / fmaxf((float)v, ief) : (float)v; };
-    double s = (double)Ns[0];
-    Os[0] = out(s);
-    const int m = nsrc < nfr ? nsrc : nfr;  // frames with a source row
-    constexpr int U = 16;
-    const int full = 1 + ((m > 1 ? m - 1 : 0) / U) * U;  // frames [1, full) in whole blocks
-    int t = 1;
-    if (full > 1) {
-        float cur[U], nxt[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = Ns[(int64_t)(1 + u) * B];
-        for (; t < full; t += U) {
-            const bool more = t + U < full;  // uniform
-            if (more) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) nxt[u] = Ns[(int64_t)(t + U + u) * B];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                s = smooth_step(mu, s, c, (double)cur[u]);
-                Os[(int64_t)(t + u) * B] = out(s);
-            }
-            if (more) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-            }
-        }
+// correctly rounded 1/x in f32 for positive normal x < 2^60: v_rcp_f32 and one
+// FMA Newton step; checked against IEEE 1.0f / x for every positive normal f32
+// in [2^-60, 2^61) (tools/micro/rcp_check.hip: 0 mismatches in 1.0e9), so it
+// equals the division it replaces (3 VALU for the ~10 of the division sequence)
+__device__ __forceinline__ float rcp_rn(float x) {
+    if (x < 0x1p60f) {
+        const float r = __builtin_amdgcn_rcpf(x);
+        return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
     }
-    for (; t < m; ++t) {
-        s = smooth_step(mu, s, c, (double)Ns[(int64_t)t * B]);
-        Os[(int64_t)t * B] = out(s);
-    }
-    for (; t < nfr; ++t) {  // the zero pad: c * 0 = +0, so s = mu s as in the general form
-        s = smooth_step(mu, s, c, 0.0);
-        Os[(int64_t)t * B] = out(s);
-    }
+    return 1.0f / x;
 }
 
-__global__ void finish_kernel(const cse_noise_job_t* __restrict__ jobs, int B,
-                              const float* __restrict__ src, float* __restrict__ dst) {
-    const cse_noise_job_t jb = jobs[blockIdx.z];
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t sig = blockIdx.y;
-    if (b >= B) return;
-    const float* Ns = src + jb.src_offset + sig * (int64_t)jb.src_frames * B + b;
-    float* Os = dst + jb.dst_offset + sig * (int64_t)jb.out_frames * B + b;
-    if (jb.inv_eps > 0.0)
-        finish_row<true>(Ns, Os, B, jb.src_frames, jb.out_frames, jb.mu, (float)jb.inv_eps);
-    else
-        finish_row<false>(Ns, Os, B, jb.src_frames, jb.out_frames, jb.mu, 0.0f);
+// One workgroup per (signal, job) row (grid n_sig x n_jobs, 256 threads):
+// tiles of F frames of the row pass through LDS, so the global side is whole
+// contiguous F x B blocks read and written by consecutive dword accesses of
+// every wave, while each thread runs its bins' recurrence over the tile from
+// LDS in numpy's order (bit-identical to the per-bin loop).  A per-bin loop
+// writing one float per frame at the 4B-byte row stride (r04's form, and a
+// flattened one-thread-per-bin form) ran the rows' stores at 2.5 TB/s; the
+// tiled block stores at 4.7 TB/s (tools/micro/row_store.hip).
+constexpr int FIN_F = 16;     // frames per tile
+constexpr int FIN_MAXU = 4;   // bins per thread (B <= 1,024)
+__global__ void __launch_bounds__(256) finish_kernel(const cse_noise_job_t* __restrict__ jobs,
+                                                     int B, const float* __restrict__ src,
+                                                     float* __restrict__ dst) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* tile = (float*)smem;  // [FIN_F][B]
+    const cse_noise_job_t jb = jobs[blockIdx.y];
+    const int64_t sig = blockIdx.x;
+    const int tid = threadIdx.x;
+    const float* Ns = src + jb.src_offset + sig * (int64_t)jb.src_frames * B;
+    float* Os = dst + jb.dst_offset + sig * (int64_t)jb.out_frames * B;
+    const int nfr = jb.out_frames, m = min(jb.src_frames, nfr);  // frames with a source row
+    const double mu = jb.mu, c = 1.0 - mu;
+    const bool inv = jb.inv_eps > 0.0;
+    const float ief = (float)jb.inv_eps;
+    double st[FIN_MAXU];
+    for (int t0 = 0; t0 < nfr; t0 += FIN_F) {
+        const int nf = min(FIN_F, nfr - t0);
+        const int nld = max(0, min(nf, m - t0)) * B;  // source floats of the tile
+        if (t0) __syncthreads();                      // the previous tile's stores have read it
+        for (int i = tid; i < nld; i += 256) tile[i] = Ns[(int64_t)t0 * B + i];
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < FIN_MAXU; ++u) {
+            const int b = tid + 256 * u;
+            if (b >= B) break;
+            double s = st[u];
+            for (int f = 0; f < nf; ++f) {
+                const int t = t0 + f;
+                const double x = t < m ? (double)tile[f * B + b] : 0.0;
+                s = t == 0 ? x : smooth_step(mu, s, c, x);  // the zero pad: c * 0 = +0
+                tile[f * B + b] = inv ? rcp_rn(fmaxf((float)s, ief)) : (float)s;
+            }
+            st[u] = s;
+        }
+        __syncthreads();
+        for (int i = tid; i < nf * B; i += 256) Os[(int64_t)t0 * B + i] = tile[i];
+    }
 }
 
 struct Workspace {
@@ -647,9 +706,9 @@ static int launch_percentile_sel(const double* P, const double* med, int64_t n_s
     double pct;
     quiet_count(T, prm, &k, &pct);
     const int n2_all = next_pow2(T), n2_sel = next_pow2(k);
-    hipLaunchKernelGGL(select_quiet_kernel, dim3((unsigned)n_sig), dim3(1024),
+    hipLaunchKernelGGL(select_quiet_kernel, dim3((unsigned)n_sig, 1u), dim3(1024),
                        (size_t)n2_all * 8 + 1024 * 4, s, (const double*)w.energy, T, n2_all, k,
-                       w.sel);
+                       w.sel, 0, (int*)nullptr);
     if (stats_wave(k, P, n_sig, T, B, STATS_PERCENTILE, (const int*)w.sel, k, pct / 100.0,
                    prm.floor_rel, eps, (double*)med, N, s)) {
         CSE_CHECK_LAUNCH("noise percentile");
@@ -823,6 +882,72 @@ extern "C" int cse_noise_percentile_med2(const double* P, const double* med, int
     return launch_percentile_sel(P, med, n_sig, T, B, prm, eps, N_b, w, s);
 }
 
+// Two percentiles x two eps values (noise_estimation.py:16-52 for each of the
+// four (percentile, eps) estimates of a hop) in four launches: one frame-energy
+// pass for both eps, one sort of each eps's energies for both percentiles, and
+// one order-statistic launch per percentile covering both eps.  Outputs equal
+// four cse_noise_percentile_med calls bit for bit.  N[p][e]: N_pe, NULL = skip.
+extern "C" int cse_noise_percentile_quad(const double* P, const double* med, int64_t n_sig, int T,
+                                         int B, double percentile_a, double percentile_b,
+                                         double eps_a, double eps_b, float* N_aa, float* N_ab,
+                                         float* N_ba, float* N_bb, void* workspace,
+                                         cse_stream_t stream) {
+    CSE_NOISE_SHAPE_CHECKS("cse_noise_percentile_quad");
+    CSE_CHECK_ARG(med && workspace, "cse_noise_percentile_quad: NULL pointer");
+    CSE_CHECK_ARG(T >= 5, "cse_noise_percentile_quad: T=%d < 5 (use the simple estimate)", T);
+    int rc = reserve_lds();
+    if (rc) return rc;
+    const hipStream_t s = (hipStream_t)stream;
+    cse_noise_params_t prm;
+    cse_noise_default_params(&prm);
+    const double pct_in[2] = {percentile_a, percentile_b};
+    int k[2];
+    double pct[2];
+    for (int p = 0; p < 2; ++p) {
+        prm.percentile = pct_in[p];
+        quiet_count(T, prm, &k[p], &pct[p]);
+    }
+    const Workspace w = carve(workspace, n_sig, T, B);
+    if (k[0] > 2048 || k[1] > 2048 || B < 16) {  // the LDS order-statistic path: one at a time
+        const double eps[2] = {eps_a, eps_b};
+        float* const N[2][2] = {{N_aa, N_ab}, {N_ba, N_bb}};
+        for (int e = 0; e < 2; ++e) {
+            launch_energy(P, n_sig, T, B, eps[e], w, s);
+            for (int p = 0; p < 2; ++p) {
+                if (!N[p][e]) continue;
+                prm.percentile = pct_in[p];
+                rc = launch_percentile_sel(P, med, n_sig, T, B, prm, eps[e], N[p][e], w, s);
+                if (rc) return rc;
+            }
+        }
+        return CSE_OK;
+    }
+    // the min-tracking IIR buffer w.S (>= 32 n_sig T bytes for B >= 16) holds
+    // the two energy rows and the four selections
+    double* en = w.S;                         // [2 eps][n_sig][T]
+    int* sel = (int*)(en + 2 * n_sig * T);    // [2 pct][2 eps][n_sig][T]
+    const int64_t ST = n_sig * (int64_t)T;
+    hipLaunchKernelGGL(frame_energy2_kernel, dim3((T + 3) / 4, (unsigned)n_sig), dim3(256), 0, s, P,
+                       T, B, eps_a, eps_b, en, en + ST);
+    const int n2_all = next_pow2(T);
+    hipLaunchKernelGGL(select_quiet_kernel, dim3((unsigned)n_sig, 2u), dim3(1024),
+                       (size_t)n2_all * 8 + 1024 * 4, s, (const double*)en, T, n2_all, k[0], sel,
+                       k[1], sel + 2 * ST);
+    float* const Ne[2][2] = {{N_aa, N_ab}, {N_ba, N_bb}};
+    for (int p = 0; p < 2; ++p) {
+        const int* sp = sel + 2 * p * ST;  // [eps][n_sig][T] of percentile p
+        StatsZ1 z1;
+        z1.sel = sp + ST;
+        z1.eps = eps_b;
+        z1.N = Ne[p][1];
+        if (!Ne[p][0] && !Ne[p][1]) continue;
+        stats_wave(k[p], P, n_sig, T, B, STATS_PERCENTILE, sp, k[p], pct[p] / 100.0, prm.floor_rel,
+                   eps_a, (double*)med, Ne[p][0], s, z1);
+    }
+    CSE_CHECK_LAUNCH("cse_noise_percentile_quad");
+    return CSE_OK;
+}
+
 extern "C" int cse_noise_min_tracking_med(const double* P, const double* med, int64_t n_sig,
                                           int T, int B, double eps, float* N, double eps_b,
                                           float* N_b, void* workspace, cse_stream_t stream) {
@@ -841,12 +966,10 @@ extern "C" int cse_noise_finish(const cse_noise_job_t* jobs, int n_jobs, int64_t
                   "cse_noise_finish: bad arguments");
     CSE_CHECK_ARG(n_sig > 0 && n_sig < 65536 && B >= 1, "cse_noise_finish: bad shape");
     if (n_jobs == 0) return CSE_OK;
-    // one workgroup per (signal, job) row, up to 1,024 threads: the row's frame
-    // writes leave one workgroup (one XCD's L2) as whole lines, where 64-bin
-    // workgroups spread a 1,028-B row over up to five XCDs
-    const int nt = row_threads(B);
-    hipLaunchKernelGGL(finish_kernel, dim3(ceil_div(B, nt), (unsigned)n_sig, (unsigned)n_jobs),
-                       dim3(nt), 0, (hipStream_t)stream, jobs, B, src, dst);
+    CSE_CHECK_ARG(B <= 256 * FIN_MAXU, "cse_noise_finish: B=%d > %d", B, 256 * FIN_MAXU);
+    const dim3 grid((unsigned)n_sig, (unsigned)n_jobs);
+    const size_t lds = (size_t)FIN_F * B * 4;
+    hipLaunchKernelGGL(finish_kernel, grid, dim3(256), lds, (hipStream_t)stream, jobs, B, src, dst);
     CSE_CHECK_LAUNCH("cse_noise_finish");
     return CSE_OK;
 }

@@ -13,6 +13,7 @@ the reference plugin's keyword arguments (parameter_ranges.py keys).
 """
 
 import ctypes
+import os
 import math
 from collections import OrderedDict
 
@@ -451,6 +452,19 @@ class GridPlan:
             for b in bases:
                 if b[1] == "percentile":
                     pc.setdefault(float(b[3]), []).append(b)
+            quad = sorted(pc) if len(pc) == 2 and not os.environ.get("CSE_NO_QUAD") else None
+            if quad and all(len(pc[e]) == 2 for e in quad) and \
+                    sorted(b[2] for b in pc[quad[0]]) == sorted(b[2] for b in pc[quad[1]]):
+                # the HEAD grid's case: two percentiles x two eps, four launches
+                # (cse_noise_percentile_quad) instead of ten
+                pa, pb = sorted(float(b[2]) for b in pc[quad[0]])
+                by = {(float(b[2]), float(b[3])): b for e in quad for b in pc[e]}
+                _lib.check(lib.cse_noise_percentile_quad(
+                    _ptr(P), _ptr(self.med), S, T, B, pa, pb, quad[0], quad[1],
+                    _ptr(raw(by[(pa, quad[0])])), _ptr(raw(by[(pa, quad[1])])),
+                    _ptr(raw(by[(pb, quad[0])])), _ptr(raw(by[(pb, quad[1])])), _ptr(self.ws), st),
+                    "cse_noise_percentile_quad")
+                pc = {}
             for eps, group in pc.items():
                 for k in range(0, len(group), 2):
                     a_, b_ = group[k], (group[k + 1] if k + 1 < len(group) else None)

@@ -199,6 +199,18 @@ int cse_noise_percentile_med(const double* P, const double* med, int64_t n_sig, 
 int cse_noise_percentile_med2(const double* P, const double* med, int64_t n_sig, int T, int B,
                               double percentile_a, double percentile_b, double eps, float* N_a,
                               float* N_b, void* workspace, cse_stream_t stream);
+/* Two percentiles x two eps values of one hop's P (the HEAD grid's four
+ * PercentileNoiseEstimator calls per hop, noise_estimation.py:16-52 with
+ * percentile_a/_b and eps_a/_b) in four launches: the frame energies for both
+ * eps from one read of P, one sort of each eps's energies for both
+ * percentiles, one order-statistic launch per percentile covering both eps.
+ * N_pe (p: percentile a/b, e: eps a/b) equal cse_noise_percentile_med bit for
+ * bit; a NULL output is skipped.  Uses the workspace's min-tracking IIR region
+ * (run it after any min-tracking call on the same stream, as the engine does). */
+int cse_noise_percentile_quad(const double* P, const double* med, int64_t n_sig, int T, int B,
+                              double percentile_a, double percentile_b, double eps_a,
+                              double eps_b, float* N_aa, float* N_ab, float* N_ba, float* N_bb,
+                              void* workspace, cse_stream_t stream);
 int cse_noise_min_tracking_med(const double* P, const double* med, int64_t n_sig, int T, int B,
                                double eps, float* N, double eps_b, float* N_b, void* workspace,
                                cse_stream_t stream);

@@ -1,4 +1,3 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-(bash tools/ab_stoi.sh libcse_r04.so libcse.so libcse_r04.so libcse.so) > gpurun_out/ab_stoi_r05a.txt 2>&1; echo "ab rc=$?"; grep -o '"ms_per_launch": [0-9.]*' gpurun_out/ab_stoi_r05a.txt
-CSE_LIB=classical_speech_enhancement_amd/libcse_stamps.so timeout -k 10 200 python tools/stoi_stages.py > gpurun_out/stoi_stages2.json 2>&1; echo "stages rc=$?"; grep -A1 '"share"\|cycles_per_cell' gpurun_out/stoi_stages2.json | grep -v "^--" | tr -d '\n'; echo
-timeout -k 10 400 python -u -m pytest tests/test_gpu_stoi.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_stoi.log 2>&1; echo "stoi tests rc=$?"; tail -2 gpurun_out/t_stoi.log
+for q in 1 2; do timeout -k 10 300 python tools/time_noise.py --reps 5 || exit 1; done > gpurun_out/time_noise_e.txt 2>&1; echo "tn rc=$?"; grep prepare gpurun_out/time_noise_e.txt
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "finish or percentile or noise" > gpurun_out/t_par.log 2>&1; echo "parity rc=$?"; tail -2 gpurun_out/t_par.log
