@@ -11,6 +11,8 @@
 // (fp64, full sorts reproducing np.percentile / np.median) over speed.
 #include "cse_common.hpp"
 
+#include <cstdlib>
+
 #include <math.h>
 
 namespace cse {
@@ -312,6 +314,125 @@ struct StatsZ1 {
     double eps = 0.0;
     float* N = nullptr;
 };
+
+// ---------------------------------------------------------------------------
+// Median over all frames by selection instead of a full sort (r05): one
+// wavefront per (bin, signal), the column's doubles as order-preserving 64-bit
+// keys in E registers per lane.  A binary descent over the key bits, counting
+// candidates with ballots, narrows the candidate set around rank r until at
+// most 64 remain (it starts at the highest bit in which the column's keys
+// differ); those are compacted into one register per lane and sorted by the
+// 64-element wave bitonic, and element r is read out.  For even T the upper
+// middle element is v1 itself when it repeats past rank T/2, else the smallest
+// key above v1.  The order statistics are the sort's exactly, so med equals
+// the bitonic path bit for bit (finite P); ~4x fewer instructions than the
+// 2,048-slot register sort at T = 1,251.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long dkey(double v) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double dval(unsigned long long k) {
+    return __builtin_bit_cast(double, (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k);
+}
+__device__ __forceinline__ unsigned long long wave_or64(unsigned long long v) {
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) v |= __shfl_xor(v, m, 64);
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_min64(unsigned long long v) {
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+        const unsigned long long o = __shfl_xor(v, m, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// the key of rank r (0-based) among the column's n real keys k[] (pads are
+// all-ones: above every real key, never of rank < n)
+template <int E>
+__device__ unsigned long long wave_select(const unsigned long long (&k)[E], int n, int r, int lane,
+                                          double* buf) {
+    // bits above the highest differing one are common to every real key
+    unsigned long long k0 = __shfl(k[0], 0, 64), dif = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        if (lane * E + e < n) dif |= k[e] ^ k0;
+    dif = wave_or64(dif);
+    int bit = dif ? 63 - __builtin_clzll(dif) : -1;
+    unsigned long long pre = k0;  // candidates: keys equal to pre above `bit`
+    int cnt = n;
+    for (; bit >= 0 && cnt > 64; --bit) {
+        const unsigned long long hi = ~((2ull << bit) - 1);  // bits above `bit` (bit 63: none)
+        const unsigned long long one = 1ull << bit;
+        int c0 = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const bool cand0 = ((k[e] ^ pre) & hi) == 0 && (k[e] & one) == 0;
+            c0 += __popcll(__ballot(cand0));
+        }
+        if (r < c0) {
+            pre &= ~one;
+            cnt = c0;
+        } else {
+            pre |= one;
+            r -= c0;
+            cnt -= c0;
+        }
+    }
+    if (cnt > 64) return pre;  // every bit decided: the candidates are all equal to pre
+    // compact the candidates (the keys equal to pre in every bit above `bit`)
+    // into buf[0, cnt), then sort 64
+    const unsigned long long hi = bit >= 0 ? ~((2ull << bit) - 1) : ~0ull;
+    int base = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        // (a pad matches a prefix of ones: only real keys are compacted)
+        const bool cand = lane * E + e < n && ((k[e] ^ pre) & hi) == 0;
+        const unsigned long long m = __ballot(cand);
+        if (cand) buf[base + __popcll(m & ((1ull << lane) - 1))] = dval(k[e]);
+        base += __popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double v[1] = {lane < cnt ? buf[lane] : INFINITY};
+    wave_bitonic<1>(v, lane);
+    return dkey(wave_at<1>(v, lane, r));
+}
+
+template <int E>
+__global__ void __launch_bounds__(256) median_select_kernel(const double* __restrict__ P, int T,
+                                                            int B, double* __restrict__ med) {
+    __shared__ double sbuf[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int b = blockIdx.x * 4 + w;
+    const int64_t sig = blockIdx.y;
+    if (b >= B) return;  // whole wavefronts only
+    const double* Ps = P + sig * (int64_t)T * B + b;
+    unsigned long long k[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        k[e] = i < T ? dkey(Ps[(int64_t)i * B]) : ~0ull;
+    }
+    const int r = (T & 1) ? T / 2 : T / 2 - 1;
+    const unsigned long long k1 = wave_select<E>(k, T, r, lane, sbuf[w]);
+    double m = dval(k1);
+    if (!(T & 1)) {  // upper middle: v1 again if it repeats past rank T/2, else the next key
+        int le = 0;
+        unsigned long long nxt = ~0ull;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            le += __popcll(__ballot(k[e] <= k1 && lane * E + e < T));
+            if (k[e] > k1 && k[e] < nxt) nxt = k[e];
+        }
+        const unsigned long long k2 = le > T / 2 ? k1 : wave_min64(nxt);
+        m = (m + dval(k2)) / 2.0;
+    }
+    if (lane == 0) med[sig * B + b] = m;
+}
 
 template <int E>
 static void launch_stats_wave(const double* P, int64_t n_sig, int T, int B, int mode,
@@ -670,6 +791,21 @@ static void quiet_count(int T, const cse_noise_params_t& prm, int* k_out, double
 
 static int launch_median(const double* P, int64_t n_sig, int T, int B, double* med,
                          hipStream_t s) {
+    static const bool sort_median = getenv("CSE_MEDIAN_SORT") != nullptr;  // A/B: the r04 sort
+    if (T >= 65 && T <= 2048 && !sort_median) {  // selection (<= 64: one bitonic anyway)
+        const dim3 g((B + 3) / 4, (unsigned)n_sig);
+        const int e = (T + 63) / 64;
+        if (e <= 8)
+            hipLaunchKernelGGL(median_select_kernel<8>, g, dim3(256), 0, s, P, T, B, med);
+        else if (e <= 16)
+            hipLaunchKernelGGL(median_select_kernel<16>, g, dim3(256), 0, s, P, T, B, med);
+        else if (e <= 24)
+            hipLaunchKernelGGL(median_select_kernel<24>, g, dim3(256), 0, s, P, T, B, med);
+        else
+            hipLaunchKernelGGL(median_select_kernel<32>, g, dim3(256), 0, s, P, T, B, med);
+        CSE_CHECK_LAUNCH("noise median");
+        return CSE_OK;
+    }
     if (stats_wave(T, P, n_sig, T, B, STATS_MEDIAN, nullptr, 0, 0.0, 0.0, 0.0, med, nullptr, s)) {
         CSE_CHECK_LAUNCH("noise median");
         return CSE_OK;

@@ -521,6 +521,52 @@ def test_percentile_pairs_equal_single_estimates(P, T_sec):
                 assert rel_l2(one[pct][s], np.ravel(ref)) < 1e-6, (T_sec, eps, s, pct)
 
 
+@pytest.mark.parametrize("T", [65, 94, 100, 626, 1251, 2048])
+def test_noise_median_exact(T):
+    """cse_noise_median (the selection kernel for 65 <= T <= 2048) equals
+    numpy's median over frames bit for bit (noise_estimation.py:34/:101-102
+    np.median): random powers over 40 binades, columns of ties, all-equal and
+    all-zero columns, odd and even T."""
+    import torch
+    from classical_speech_enhancement_amd import _lib
+    from classical_speech_enhancement_amd.engine import Engine, _ptr, _stream
+    lib = Engine().lib
+    rng = np.random.default_rng(T)
+    S, B = 3, 257
+    P = 10.0 ** rng.uniform(-12, 3, size=(S, T, B))
+    P[0, :, 1] = 0.5                                     # all equal
+    P[0, :, 2] = 0.0                                     # all zero
+    P[1, :, 3] = rng.integers(0, 4, T) * 0.25            # heavy ties
+    P[1, :, 4] = np.where(rng.random(T) < 0.6, 1e-10, P[1, :, 4])  # a floor shared by most frames
+    P[2, :, 5] = np.arange(T)[::-1] * 1e-3               # monotone
+    Pd = torch.as_tensor(P).cuda()
+    med = torch.empty((S, B), dtype=torch.float64, device="cuda")
+    _lib.check(lib.cse_noise_median(_ptr(Pd), S, T, B, _ptr(med), _stream()), "median")
+    ref = np.median(P, axis=1)
+    got = med.cpu().numpy()
+    assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
+
+
+@pytest.mark.parametrize("n_fft,sec", [(512, 0.75), (1024, 0.75), (512, 10.0), (1024, 10.0)])
+def test_noise_median_exact_on_stft(n_fft, sec):
+    """The same on STFT powers of speech-like pairs (the engine's own P: ties
+    from the reflect padding, columns spanning a few binades, the pad lanes of a
+    short column sharing the keys' prefix), T = 94 and 1,251 frames."""
+    import torch
+    from classical_speech_enhancement_amd import _lib
+    from classical_speech_enhancement_amd.engine import Engine, _ptr, _stream
+    eng = Engine()
+    clean, noisy = make_pair(6, sec)
+    x = torch.as_tensor(np.stack([noisy, clean, noisy - clean])).cuda()
+    _, Pw = eng.stft(x, n_fft, 128, want_y=False)
+    S, T, B = Pw.shape
+    med = torch.empty((S, B), dtype=torch.float64, device="cuda")
+    _lib.check(eng.lib.cse_noise_median(_ptr(Pw), S, T, B, _ptr(med), _stream()), "median")
+    ref = np.median(Pw.cpu().numpy(), axis=1)
+    got = med.cpu().numpy()
+    assert np.array_equal(got, ref), (T, B, np.argwhere(got != ref)[:5])
+
+
 @pytest.mark.parametrize("T_sec", [1.0, 20.0])
 def test_percentile_quad_equals_single_estimates(P, T_sec):
     """cse_noise_percentile_quad (two percentiles x two eps in four launches)
