@@ -263,7 +263,12 @@ class TimedJob:
         self.units = self.mps[0].units
         self.n_cells = len(specs)
         self.main_s = torch.cuda.current_stream()
-        self.prep_s = torch.cuda.Stream() if n_buf > 1 else self.main_s
+        # the analysis side stream at high priority (r05): with every analysis
+        # workgroup small enough to take the place of one finished enhance
+        # workgroup (cse_stft.hip), its launches are dispatched into the
+        # running enhance launch's freed slots instead of waiting for its drain
+        prio = int(os.environ.get("CSE_PREP_PRIORITY", "-1"))
+        self.prep_s = torch.cuda.Stream(priority=prio) if n_buf > 1 else self.main_s
         self.ev_prep = [torch.cuda.Event() for _ in range(n_buf)]
         self.ev_done = [None] * n_buf
         self.k = 0
