@@ -53,7 +53,12 @@ constexpr int CST = 128;                 // coefficient row stride
 constexpr int FR = 256, HOP = 128;       // frames at 10 kHz
 constexpr int NBAND = 15, NSEG = 30;
 constexpr int FB = 16;                   // most STFT frames per phase-A block
-constexpr int MAXD = 28;                 // most distinct 10-kHz half-blocks per block
+// most distinct 10-kHz half-blocks per block: 16 consecutive kept frames need
+// 17, so only blocks around dropped frames hold fewer than FB frames (r05: 28
+// before; 4,096 cells 4.35 / 4.44 -> 4.24 / 4.31 ms, profiles/r05_ab_stoi_maxd.txt.
+// Staging the samples as f64 instead, converted once rather than by each
+// phase group, measured 4.94 / 4.99 ms: not kept)
+constexpr int MAXD = 18;
 // block table (ints): D, j0, nf, p[MAXD], sa[FB + 1], sb[FB + 1].  A block takes
 // frames while nf <= FB and its OLA rows need <= MAXD distinct half-blocks
 // (a row needs at most 2, so every block but the last has >= 13 frames)
