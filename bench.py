@@ -263,11 +263,13 @@ class TimedJob:
         self.units = self.mps[0].units
         self.n_cells = len(specs)
         self.main_s = torch.cuda.current_stream()
-        # the analysis side stream at high priority (r05): with every analysis
-        # workgroup small enough to take the place of one finished enhance
-        # workgroup (cse_stft.hip), its launches are dispatched into the
-        # running enhance launch's freed slots instead of waiting for its drain
-        prio = int(os.environ.get("CSE_PREP_PRIORITY", "-1"))
+        # the analysis side stream (priority: CSE_PREP_PRIORITY, default 0).  Its
+        # first STFT (80 KB of LDS) cannot take the slot of one finished enhance
+        # workgroup, so the chain starts in the launch's drain tail, where the
+        # freed CUs are idle anyway; r05 measured the chain inside the launch
+        # (STFT at 47 KB, priority -1): no faster at 512, 4 % slower at 1024
+        # ("analysis overlap")
+        prio = int(os.environ.get("CSE_PREP_PRIORITY", "0"))
         self.prep_s = torch.cuda.Stream(priority=prio) if n_buf > 1 else self.main_s
         self.ev_prep = [torch.cuda.Event() for _ in range(n_buf)]
         self.ev_done = [None] * n_buf

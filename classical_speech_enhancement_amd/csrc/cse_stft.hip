@@ -27,9 +27,7 @@ __device__ __forceinline__ int64_t reflect_index(int64_t p, int64_t len) {
 // sincospi / cospi per point), and only frames that reach past either end of
 // the signal take the 64-bit reflect arithmetic.  Every element sees the same
 // operations as before, so Y and P are bit-identical to the one-frame form.
-// Two frames per workgroup (r05; four before): 48 KB of LDS, which fits the
-// slot one finished n_fft = 1024 enhance workgroup (52.8 KB) leaves.
-constexpr int STFT_FPB = 2;
+constexpr int STFT_FPB = 4;
 template <int NFFT>
 __global__ void __launch_bounds__(256) stft_kernel(const double* __restrict__ x,
                                                    const double* __restrict__ x_sub,
@@ -178,11 +176,6 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// LDS: the exchanges move one component at a time through a 16 x 17 double
-// block per frame (r05: the complex block took the workgroup to 80 KB, which
-// cannot take the place of one finished enhance workgroup — 53.6 KB — so a
-// step's analysis waited for the previous enhance launch to drain; at 46.8 KB
-// it is dispatched into the enhance launch's freed slots)
 constexpr int S512_FPB = 16;  // frames per workgroup (4 per wavefront)
 __global__ void __launch_bounds__(256) stft512_kernel(const double* __restrict__ x,
                                                       const double* __restrict__ x_sub,
@@ -190,7 +183,7 @@ __global__ void __launch_bounds__(256) stft512_kernel(const double* __restrict__
                                                       float2* __restrict__ Y,
                                                       double* __restrict__ P) {
     constexpr int M = 256, NF = 512, B = 257;
-    __shared__ double buf[S512_FPB][M + 16];  // 16 x 17: the transposed reads of 16 lanes spread banks
+    __shared__ dcx buf[S512_FPB][M + 16];  // +16: the transposed reads of 16 lanes spread banks
     __shared__ dcx tw256[M], tw512[M];
     __shared__ double win[NF];
     const int tid = threadIdx.x;
@@ -211,7 +204,7 @@ __global__ void __launch_bounds__(256) stft512_kernel(const double* __restrict__
     const double* xd = x_sub ? x_sub + sig * len : nullptr;
     const int64_t p0 = (int64_t)t * hop - NF / 2;
     const bool inside = p0 >= 0 && p0 + NF <= len;
-    double* fb = buf[fl];
+    dcx* fb = buf[fl];
     // pass 1: lane m2 = lane loads z[16 m1 + m2] = xw[32 m1 + 2 m2 + (0, 1)]
     dcx v[16];
 #pragma unroll
@@ -232,34 +225,21 @@ __global__ void __launch_bounds__(256) stft512_kernel(const double* __restrict__
     for (int k1 = 1; k1 < 16; ++k1) v[k1] = dmul(v[k1], tw256[(lane * k1) & (M - 1)]);
     // transpose: entry (m2, k1) at fb[k1 * 17 + m2]
 #pragma unroll
-    for (int k1 = 0; k1 < 16; ++k1) fb[k1 * 17 + lane] = v[k1].x;  // real parts, then imaginary
-    double part[16];
+    for (int k1 = 0; k1 < 16; ++k1) fb[k1 * 17 + lane] = v[k1];
     wave_lds_sync();
 #pragma unroll
-    for (int m2 = 0; m2 < 16; ++m2) part[m2] = fb[lane * 17 + m2];
-    wave_lds_sync();
-#pragma unroll
-    for (int k1 = 0; k1 < 16; ++k1) fb[k1 * 17 + lane] = v[k1].y;
-    wave_lds_sync();
-#pragma unroll
-    for (int m2 = 0; m2 < 16; ++m2) v[m2] = dmk(part[m2], fb[lane * 17 + m2]);
+    for (int m2 = 0; m2 < 16; ++m2) v[m2] = fb[lane * 17 + m2];
     fdft16(v);  // v[k2] = Z[k1 + 16 k2], k1 = lane
     wave_lds_sync();
 #pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) fb[lane + 16 * k2] = v[k2].x;  // natural index k, real parts
-    wave_lds_sync();
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) part[k2] = fb[(M - lane - 16 * k2) & (M - 1)];
-    wave_lds_sync();
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) fb[lane + 16 * k2] = v[k2].y;
+    for (int k2 = 0; k2 < 16; ++k2) fb[lane + 16 * k2] = v[k2];  // natural index k
     wave_lds_sync();
     const int64_t row = (sig * T + t) * (int64_t)B;
 #pragma unroll
     for (int k2 = 0; k2 < 16; ++k2) {
         const int k = lane + 16 * k2;
         const dcx z = v[k2];
-        const dcx w = dmk(part[k2], fb[(M - k) & (M - 1)]);  // Z_{M-k} (Z_0 for k = 0)
+        const dcx w = fb[(M - k) & (M - 1)];  // Z_{M-k} (Z_0 for k = 0)
         // E = (z + conj w)/2, O = (z - conj w)/(2i)
         const dcx e = dmk(0.5 * (z.x + w.x), 0.5 * (z.y - w.y));
         const dcx o = dmk(0.5 * (z.y + w.y), -0.5 * (z.x - w.x));
