@@ -95,3 +95,19 @@ def test_batched_cells_lag_and_clip(dev):
         e = _shift_fit_clip(outs[c].astype(np.float64), lags[c], L)
         ora = stoi_ref.stoi(clean[sig[c]], e, 16000)
         assert abs(got[c] - ora) < TOL, (c, lags[c], got[c], ora)
+
+
+def test_fragmented_silence(dev):
+    """A clean signal of 30-ms bursts every 70 ms, silent (40 dB down) in
+    between: the silent-frame mask drops frames all along, so the phase-A
+    blocks fill their distinct-half-block budget (18, r05) with few frames
+    and split often; device = oracle."""
+    rng = np.random.default_rng(21)
+    n = 16000 * 4
+    t = np.arange(n)
+    burst = ((t % 1120) < 480).astype(np.float64)
+    clean = rng.standard_normal(n) * (burst + 1e-4)
+    for test in (clean + 0.1 * rng.standard_normal(n), 0.5 * clean):
+        got = dev.calculate_stoi(clean, test, 16000)
+        ora = stoi_ref.calculate_stoi(clean, test.astype(np.float32).astype(np.float64), 16000)
+        assert abs(got - ora) < TOL, (got, ora)
