@@ -320,8 +320,13 @@ class TimedJob:
             if self.prep_evs is not None:  # timed region: the analysis chain's span
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record(self.prep_s)
+            # every plan's STFTs, then every plan's noise chains (GridPlan.prepare_stft)
+            # (full grid, A/B on one box: 571.2 / 572.3 ms/step against 575.4 /
+            # 572.8 with each plan's STFTs and chains in turn)
             for p in self.mps[b].plans:
-                p.prepare(self.noisy, self.clean)
+                p.prepare_stft(self.noisy, self.clean)
+            for p in self.mps[b].plans:
+                p.prepare_noise(self.clean)
             if ev is not None:
                 ev[1].record(self.prep_s)
                 self.prep_evs.append(ev)
