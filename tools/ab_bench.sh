@@ -3,7 +3,7 @@
 # each a fresh process; prints ms_per_step, the enhance-kernel ms and the
 # analysis chain's span per variant.  Optional parity tests first ($TESTS).
 #   VARIANTS="CSE_PREP_PRIORITY=-1 CSE_PREP_PRIORITY=0" bash tools/ab_bench.sh
-# (a variant is one NAME=VALUE word, or "-" for the plain environment)
+# (a variant is NAME=VALUE[,NAME=VALUE...], or "-" for the plain environment)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 if [ -n "$TESTS" ]; then
@@ -21,7 +21,7 @@ for r in $(seq ${ROUNDS:-2}); do
     if [ "$v" = "-" ]; then
       timeout -k 10 ${LIMIT:-300} python bench.py $B > $out 2> $out.err || { echo "$v failed"; tail -5 $out.err; exit 1; }
     else
-      env "$v" timeout -k 10 ${LIMIT:-300} python bench.py $B > $out 2> $out.err || { echo "$v failed"; tail -5 $out.err; exit 1; }
+      env ${v//,/ } timeout -k 10 ${LIMIT:-300} python bench.py $B > $out 2> $out.err || { echo "$v failed"; tail -5 $out.err; exit 1; }
     fi
     python - "$out" "$v" <<'EOF'
 import json, sys
