@@ -765,6 +765,7 @@ def roofline_block(n_fft, units, kern_ms):
                                   "counter": ("SQ_INSTS_VALU_FLOPS_FP32 x 64: the counter counts per "
                                               "wave-instruction, weighted by FLOPs per lane")}
         for k in ("share_wait_inst_any", "share_wait_any", "share_wait_inst_lds",
+                  "share_active_inst_valu", "share_active_inst_any",
                   "lds_array_busy", "lds_conflict_cycles_per_lds_inst", "vgprs", "waves_per_simd"):
             if pmc.get(k) is not None:
                 roof[k] = pmc[k]

@@ -181,6 +181,8 @@ def main(tag, rnd, units512=None, units1024=None):
                "waves_per_simd": k.get("waves_per_simd"),
                "share_wait_inst_any": k.get("share_wait_inst_any"),
                "share_wait_any": k.get("share_wait_any"),
+               "share_active_inst_valu": k.get("share_active_inst_valu"),
+               "share_active_inst_any": k.get("share_active_inst_any"),
                "lds_conflict_cycles_per_lds_inst": k.get("lds_conflict_cycles_per_lds_inst"),
                "lds_array_busy": k.get("lds_array_busy"),
                "share_wait_inst_lds": k.get("share_wait_inst_lds"),
