@@ -31,6 +31,9 @@
 #ifndef CSE_PK
 #define CSE_PK 1  // n_fft 512: packed f32 (v_pk_*) gain pairs, packing and DFTs
 #endif
+#ifndef CSE_ROWS_BUF
+#define CSE_ROWS_BUF 0
+#endif
 #ifndef CSE_PK_1024
 #define CSE_PK_1024 0  // the same at n_fft 1024 (r04: 53.3 against 52.8 ms at 13 pairs, so off)
 #endif
@@ -71,6 +74,37 @@ struct Args {
 
 #ifdef CSE_MARKS  // static instruction-count analysis builds only (tools/isa_sections.py)
 #define CSE_MARK(name) asm volatile(";#MARK " name)
+#elif defined(CSE_ENH_STAMPS)
+// Per-stage timing (analysis builds only, tools/enhance_stages.py): at each
+// stage marker, the shader cycles (s_memtime) since the previous marker go to
+// the stage that just ended; wave 0 of every workgroup stores its sums, the
+// (hop, algorithm) of the group beside them, into the buffer
+// cse_enhance_stamp_buffer() installs
+//   0 barrier + loop top   1 gain   2 mirror exchange   3 row staging
+//   4 pass-1 DFT           5 transpose + pass-2 DFT      6 window    7 retire
+static __device__ unsigned long long* g_enh_stamps;  // per translation unit
+struct EnhStamps {
+    unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long last = 0;
+    __device__ void start() { last = __builtin_amdgcn_s_memtime(); }
+    // the scheduling barriers keep each stage's instructions on their side of
+    // the stamp (without them the compiler moved pass-1 arithmetic above the
+    // pass-1 marker); the stamps still cost the waits they force
+    __device__ void mark(int ended) {
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+        acc[ended] += now - last;
+        last = now;
+    }
+};
+// the stage that ends at marker `name` (the markers are string literals)
+__device__ constexpr int enh_stage_before(const char* n) {
+    return n[0] == 'g' ? 0 : n[0] == 'x' ? 1 : (n[0] == 'r' && n[1] == 'o') ? 2
+         : (n[0] == 'p' && n[4] == '1') ? 3 : n[0] == 'p' ? 4 : n[0] == 'w' ? 5
+         : n[0] == 'r' ? 6 : 7;
+}
+#define CSE_MARK(name) est.mark(enh_stage_before(name))
 #else
 #define CSE_MARK(name)
 #endif
@@ -882,7 +916,42 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
     // clean samples stay f64 in flight: converting at load time made the
     // compiler wait (vmcnt(0)) for every row load right after issuing them
     double pc[W::CPT];
+#if CSE_ROWS_BUF
+    // the row loads through buffer resources (r05): an index past a row's end
+    // returns 0 instead of taking a per-lane branch.  Y: the workgroup's nf
+    // frames; N: the same for a time-varying row, the static row itself
+    // re-read every frame when nstride = 0; clean: [0, len), so the clean
+    // samples outside the signal are 0 without the range test (a NULL clean
+    // has no records).  Offsets go through opaque_off: a constant folded into
+    // the instruction's immediate field would escape the range check.
+    const __amdgpu_buffer_rsrc_t yrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)Ybase, (short)0, nf * B * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t nrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)Nbase, (short)0, (nstride ? (nf - 1) * nstride + B : B) * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t crc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)cbase, (short)0, cbase ? len * 8 : 0, 0x00020000);
+#endif
     auto load_rows = [&](int t) {  // issue loads of frame t's rows into registers
+#if CSE_ROWS_BUF
+        if (t < nf) {
+#pragma unroll
+            for (int u = 0; u < W::YPT; ++u) {
+                const int k = tid + u * W::THREADS;  // k >= B: not stored (store_rows)
+                py[u] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(
+                    yrc, opaque_off(8 * (t * B + k)), 0, 0));
+                pn[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                    nrc, opaque_off(4 * (t * nstride + k)), 0, 0));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < W::CPT; ++u) {
+            const int j = tid + u * W::THREADS;
+            const int o = t * HOP - NFFT / 2 + j + lag;  // clean sample scored against y[o - lag]
+            if (j < HOP)  // uniform per wave
+                pc[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                    crc, opaque_off(8 * o), 0, 0));
+        }
+#else
         if (t < nf) {
 #pragma unroll
             for (int u = 0; u < W::YPT; ++u) {
@@ -899,6 +968,7 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
             const int o = t * HOP - NFFT / 2 + j + lag;  // clean sample scored against y[o - lag]
             pc[u] = (j < HOP && cbase && o >= 0 && o < len) ? cbase[o] : 0.0;
         }
+#endif
     };
     // rows of frame t live in buffer t&1: Y and gamma = max(|Y|^2 inv, eps)
     // (the noise row itself for SS); at 512 also d = max(gamma - 1, 0) and
@@ -1001,6 +1071,10 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
     double sse = 0.0;
     float chk = 0.0f;  // sum of y*0 over retired samples: NaN iff some y is not finite
 
+#ifdef CSE_ENH_STAMPS
+    EnhStamps est;
+    est.start();
+#endif
     for (int t = 0; t < nf + R - 1; ++t) {
         float x[32];  // this frame's windowed IFFT samples (0 in flush frames)
         f2 xp[16];    // CSE_PK: the same as pairs (x[2p], x[2p + 1])
@@ -1476,6 +1550,15 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
     const unsigned long long bad = __ballot(chk != 0.0f);  // NaN != 0
     const unsigned long long my = (bad >> (cs * L)) & ((1ull << L) - 1);
     const int64_t cell_idx = (int64_t)(wcell - a.cells) + cslot;
+#ifdef CSE_ENH_STAMPS
+    if (tid == 0 && g_enh_stamps) {
+        unsigned long long* o = g_enh_stamps + (int64_t)blockIdx.x * 10;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = est.acc[k];
+        o[8] = ALGO;
+        o[9] = HOP;
+    }
+#endif
     if (i == 0 && valid) {
         if (a.sse) a.sse[cell_idx] = sse;
         if (a.finite) a.finite[cell_idx] = my == 0 ? 1 : 0;
@@ -1545,6 +1628,20 @@ const void* enhance_fn_512(bool out);  // cse_enhance_512.hip
 #endif
 
 }  // namespace cse
+
+#ifdef CSE_ENH_STAMPS
+// analysis builds only: per-workgroup stage cycles into buf [n_groups][10]
+// (u64: 8 stages, algorithm, hop) of this translation unit's n_fft, or off (NULL)
+#if !defined(CSE_ENHANCE_ONLY) || CSE_ENHANCE_ONLY == 512
+extern "C" int cse_enhance_stamp_buffer_512(void* buf) {
+#else
+extern "C" int cse_enhance_stamp_buffer_1024(void* buf) {
+#endif
+    unsigned long long* p = (unsigned long long*)buf;
+    return hipMemcpyToSymbol(HIP_SYMBOL(cse::g_enh_stamps), &p, sizeof(p)) == hipSuccess ? CSE_OK
+                                                                                          : CSE_ELAUNCH;
+}
+#endif
 
 #if !defined(CSE_ENHANCE_ONLY) || CSE_ENHANCE_ONLY == 1024
 using namespace cse;
