@@ -31,8 +31,14 @@
 #ifndef CSE_PK
 #define CSE_PK 1  // n_fft 512: packed f32 (v_pk_*) gain pairs, packing and DFTs
 #endif
+// row loads through buffer resources, branch-free (r05, 13 pairs, three
+// alternating rounds: 512 22.50 / 22.51 / 22.51 -> 22.06 / 22.09 / 22.10 ms;
+// 1024 55.5 / 55.3 against 54.9 / 55.3 ms, so 1024 keeps the masked loads)
 #ifndef CSE_ROWS_BUF
-#define CSE_ROWS_BUF 0
+#define CSE_ROWS_BUF 1
+#endif
+#ifndef CSE_ROWS_BUF_1024
+#define CSE_ROWS_BUF_1024 0
 #endif
 #ifndef CSE_PK_1024
 #define CSE_PK_1024 0  // the same at n_fft 1024 (r04: 53.3 against 52.8 ms at 13 pairs, so off)
@@ -916,23 +922,29 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
     // clean samples stay f64 in flight: converting at load time made the
     // compiler wait (vmcnt(0)) for every row load right after issuing them
     double pc[W::CPT];
-#if CSE_ROWS_BUF
-    // the row loads through buffer resources (r05): an index past a row's end
-    // returns 0 instead of taking a per-lane branch.  Y: the workgroup's nf
-    // frames; N: the same for a time-varying row, the static row itself
-    // re-read every frame when nstride = 0; clean: [0, len), so the clean
-    // samples outside the signal are 0 without the range test (a NULL clean
-    // has no records).  Offsets go through opaque_off: a constant folded into
-    // the instruction's immediate field would escape the range check.
+    constexpr bool ROWS_BUF = NFFT == 512 ? CSE_ROWS_BUF : CSE_ROWS_BUF_1024;
+    // ROWS_BUF: the row loads through buffer resources (r05): an index past a
+    // row's end returns 0 instead of taking a per-lane branch.  Y: the
+    // workgroup's nf frames; N: the same for a time-varying row, the static row
+    // itself re-read every frame when nstride = 0; clean: [0, len), so the
+    // clean samples outside the signal read 0 without the range test
+    // (negative offsets wrap to huge unsigned values; a NULL clean has no
+    // records).  Offsets go through opaque_off: a constant folded into the
+    // instruction's immediate field would escape the range check.  One
+    // resource per array, not per row and frame (per-frame resources measured
+    // 22.46 against 22.58 ms, per-array 22.08 against 22.51; per-array with a
+    // workgroup-uniform fallback to the masked loads for rows past 2 GiB
+    // 23.24 against 22.53).  Byte offsets are 32-bit: the entry point takes
+    // n_fft 512 signals whose spectrum rows stay below 2 GiB (cse.h).
     const __amdgpu_buffer_rsrc_t yrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)Ybase, (short)0, nf * B * 8, 0x00020000);
+        (void*)Ybase, (short)0, ROWS_BUF ? nf * B * 8 : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t nrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)Nbase, (short)0, (nstride ? (nf - 1) * nstride + B : B) * 4, 0x00020000);
+        (void*)Nbase, (short)0, ROWS_BUF ? ((nstride ? (nf - 1) * nstride : 0) + B) * 4 : 0,
+        0x00020000);
     const __amdgpu_buffer_rsrc_t crc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)cbase, (short)0, cbase ? len * 8 : 0, 0x00020000);
-#endif
+        (void*)cbase, (short)0, ROWS_BUF && cbase ? len * 8 : 0, 0x00020000);
     auto load_rows = [&](int t) {  // issue loads of frame t's rows into registers
-#if CSE_ROWS_BUF
+      if constexpr (ROWS_BUF) {
         if (t < nf) {
 #pragma unroll
             for (int u = 0; u < W::YPT; ++u) {
@@ -951,7 +963,7 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                 pc[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
                     crc, opaque_off(8 * o), 0, 0));
         }
-#else
+      } else {
         if (t < nf) {
 #pragma unroll
             for (int u = 0; u < W::YPT; ++u) {
@@ -968,7 +980,7 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
             const int o = t * HOP - NFFT / 2 + j + lag;  // clean sample scored against y[o - lag]
             pc[u] = (j < HOP && cbase && o >= 0 && o < len) ? cbase[o] : 0.0;
         }
-#endif
+      }
     };
     // rows of frame t live in buffer t&1: Y and gamma = max(|Y|^2 inv, eps)
     // (the noise row itself for SS); at 512 also d = max(gamma - 1, 0) and
@@ -1658,6 +1670,12 @@ extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells
     CSE_CHECK_ARG(cells && Y && noise, "cse_enhance_cells: NULL cells/Y/noise");
     CSE_CHECK_ARG(len >= 1 && len < (1ll << 30) && n_cells >= 0,
                   "cse_enhance_cells: len=%lld n_cells=%lld", (long long)len, (long long)n_cells);
+    // n_fft 512 reads its rows through buffer resources with 32-bit byte
+    // offsets (CSE_ROWS_BUF): the signal's spectrum rows at the smallest hop
+    // must stay below 2 GiB
+    CSE_CHECK_ARG(n_fft != 512 || !CSE_ROWS_BUF || (1 + len / 128) * 257 * 8 < (1ll << 31),
+                  "cse_enhance_cells: len=%lld too long for n_fft=512 (spectrum rows >= 2 GiB)",
+                  (long long)len);
     if (n_cells == 0) return CSE_OK;
     Args a;
     a.len = len;

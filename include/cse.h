@@ -265,7 +265,9 @@ int cse_istft_norm(int n_fft, int hop, int64_t len, float* out, cse_stream_t str
  * Optional outputs: y_out (the first out_len samples of the enhanced waveform,
  * f32, at out_offset; out_len = len for the whole waveform) and g_out (the
  * gain matrix, f32 [T][B] at gain_offset).
- * n_fft in {512, 1024}; hop in {128, 256}.
+ * n_fft in {512, 1024}; hop in {128, 256}; len < 2^30, and at n_fft 512
+ * (1 + len/128) * 257 * 8 < 2^31 (len < 133.6 M samples, 2.3 h at 16 kHz:
+ * its rows are read with 32-bit byte offsets).  noise_stride is 0 or B.
  */
 int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
                       const float* Y, const float* noise, const double* clean,

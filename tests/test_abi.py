@@ -46,6 +46,16 @@ def test_version_and_error_channel(lib):
     rc = lib.cse_noise_estimate(7, ctypes.c_void_p(16), 1, 100, 257, 20.0, 1e-10,
                                 ctypes.c_void_p(16), ctypes.c_void_p(16), None)
     assert rc == -1 and b"Unbekannte Methode" in lib.cse_last_error()
+    # n_fft 512 rows are read with 32-bit byte offsets (cse.h): the longest
+    # signal is (1 + len/128) * 257 * 8 < 2^31; n_fft 1024 takes up to 2^30
+    ok512 = ((2**31 - 1) // (257 * 8) - 1) * 128 + 127
+    rc = lib.cse_enhance_cells(512, ok512 + 1, ctypes.c_void_p(16), 0, ctypes.c_void_p(16),
+                               ctypes.c_void_p(16), None, None, 0, None, None, None, None)
+    assert rc == -1 and b"too long for n_fft=512" in lib.cse_last_error()
+    for n_fft, n in ((512, ok512), (1024, ok512 + 1)):  # n_cells = 0: checked, nothing launched
+        rc = lib.cse_enhance_cells(n_fft, n, ctypes.c_void_p(16), 0, ctypes.c_void_p(16),
+                                   ctypes.c_void_p(16), None, None, 0, None, None, None, None)
+        assert rc == 0, lib.cse_last_error()
 
 
 def test_cells_per_group_matches_header(lib):
