@@ -74,8 +74,17 @@ constexpr int SROW = 43;                 // staging: 8 rows (sample mod 8) x 43 
 // reads of lane tid = 27 s + g fall on bank tid + const (mod 64), so the
 // slots sharing a wave do not collide (344 collided on 3 banks per slot
 // boundary; 4,096 cells 4.30 / 4.35 -> 4.29 / 4.28 ms)
-constexpr int SSTR = 347;
-static_assert(SSTR >= 8 * SROW && SSTR % 64 == GRP, "staging slot stride");
+#ifndef CSE_STOI_LIN
+#define CSE_STOI_LIN 1
+#endif
+// CSE_STOI_LIN (r05): the slot's samples in order, st[uu], so a phase group's 8
+// samples of one tap block are 32 contiguous, aligned bytes: two ds_read_b128
+// instead of eight ds_read_b32 per block (the slot stride a multiple of 16 B).
+// 4,096 10-s cells, two alternating rounds: 4.55 / 4.50 -> 4.24 / 4.30 ms.
+// (CSE_STOI_LIN=0: 8 rows by sample mod 8, the stride below)
+constexpr int SSTR = CSE_STOI_LIN ? 344 : 347;
+static_assert(CSE_STOI_LIN ? (SSTR >= 8 * (GRP + 15) + 8 && SSTR % 4 == 0)
+                           : (SSTR >= 8 * SROW && SSTR % 64 == GRP), "staging slot stride");
 // (r03's opt-in i8-sliced resampler on the matrix pipe, level with this fp64 FIR
 // at best, left the product in r04: tools/stoi_mf.md says how to rebuild it)
 constexpr int STAGE_F = SLOTS * SSTR;
@@ -531,7 +540,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                         const int uu = fr + FW * u;
                         float v = (unsigned)(fbase + FW * u) < (unsigned)cnt ? pre[u] : 0.0f;
                         if (clip) v = fminf(fmaxf(v, -1.0f), 1.0f);
-                        if (u < PF - 1 || uu < NU) st[(uu & 7) * SROW + (uu >> 3)] = v;
+                        if (u < PF - 1 || uu < NU) st[CSE_STOI_LIN ? uu : (uu & 7) * SROW + (uu >> 3)] = v;
                     }
                 }
                 __syncthreads();  // stage (and the next block's table) visible
@@ -545,7 +554,9 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                     const int64_t p = tb[T_P + c0 + s];
                     const int64_t q0 = (HOP * p) / UP;
                     const int64_t q = q0 + g;
-                    const float* st = L.u.a.stage + s * SSTR + g;
+                    const float* st = L.u.a.stage + s * SSTR + (CSE_STOI_LIN ? 8 * g : g);
+                    // sample j of tap block kb (j < 8): st[8 kb + j] (LIN) or st[j SROW + kb]
+                    auto sidx = [](int kb, int j) { return CSE_STOI_LIN ? 8 * kb + j : j * SROW + kb; };
                     double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
                     // taps kk = 8 kb + j of phase r; c_r[kk] = 0 outside
                     // 8r <= 5kk <= 8r + 580 (and kk >= 123): the edge blocks
@@ -555,7 +566,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
 #pragma unroll
                         for (int j = 0; j < 8; ++j) {
                             const int kk = 8 * kb + j;
-                            const double e = (double)st[j * SROW + kb];
+                            const double e = (double)st[sidx(kb, j)];
 #pragma unroll
                             for (int r = 0; r < 5; ++r)
                                 if (5 * kk >= 8 * r && 5 * kk <= 8 * r + 580)
@@ -572,7 +583,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                     // scalar load plus four LDS round trips
                     float sv[8];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) sv[j] = st[j * SROW + 1];
+                    for (int j = 0; j < 8; ++j) sv[j] = st[sidx(1, j)];
                     taps(std::integral_constant<int, 0>());
 #pragma unroll 1
                     for (int kb = 1; kb < 14; ++kb) {  // every tap nonzero
@@ -583,7 +594,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                         for (int r = 0; r < 5; ++r) acc[r] = fma(coef[r * CST + 8 * kb], e[0], acc[r]);
                         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                        for (int j = 0; j < 8; ++j) sv[j] = st[j * SROW + kb + 1];
+                        for (int j = 0; j < 8; ++j) sv[j] = st[sidx(kb + 1, j)];
                         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                         for (int j = 1; j < 8; ++j) {
