@@ -532,7 +532,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
         } else {
             for (int c0 = 0; c0 < D; c0 += NSL) {
                 const int ns = min(NSL, D - c0);
-                // stage e[8 q0 - 58 + uu], uu < 339, at [uu & 7][uu >> 3]
+                // stage e[8 q0 - 58 + uu], uu < 339, at [uu] (LIN) or [uu & 7][uu >> 3]
                 if (fs < ns) {
                     float* st = L.u.a.stage + fs * SSTR;
 #pragma unroll
