@@ -25,9 +25,9 @@ The line also carries two labelled blocks beside the headline:
   sweep         the reference's whole job through search.run_grid: alignment,
                 SNR and STOI of every cell, the gather and both sequential
                 selections, wall seconds and cells/s;
-and "roofline", the enhance kernel against VALU issue (the resource it
-spends), with the measured HBM GB/s and SURVEY §8(d)'s algorithmic byte
-figure beside it.
+and "roofline", the enhance kernel against VALU lane-op throughput (the
+resource it spends: each instruction priced at the SIMD cycles it takes), with
+the measured HBM GB/s and SURVEY §8(d)'s algorithmic byte figure beside it.
 
 At N = 1 the line also carries
   parity        the timed step's per-cell SNR table of pair 0 against the
@@ -55,13 +55,12 @@ sys.path.insert(0, REPO)
 METRIC = ("STFT frame-gain evals/sec/node, 16kHz 512-pt FFT full grid; 1/2/4/8-GPU scaling")
 HBM_PEAK = 8.0e12              # MI355X_MICROARCH.md: 8.0 TB/s spec
 SIMDS = 1024                   # 256 CUs x 4 SIMD-32
-# what a dense, dependency-free VALU stream sustains per SIMD, in shader cycles
-# per wave-instruction (tools/micro/valu_peak.hip, profiles/r05_micro_valu_peak.txt),
-# by waves per SIMD: {waves: (v_fma_f32, v_pk_fma_f32, v_exp_f32)}
-DENSE_CYC = {1: (9.02, 7.52, 21.64), 2: (5.13, 4.70, 7.61), 3: (3.98, 3.76, 6.37),
-             4: (3.46, 3.31, 5.76), 6: (2.95, 2.86, 5.16), 8: (2.71, 2.64, 4.86)}
-FP32_PEAK = 157.3e12           # MI355X_MICROARCH.md: FP32 vector, spec
-VALU_CYC, TRANS_CYC = 2, 4     # wave64 issue cycles: v_fma_f32 (SIMD-32), transcendental (2x: tools/micro/valu_rate.hip)
+FP32_PEAK = 157.3e12           # MI355X_MICROARCH.md: FP32 vector, spec (64 FLOP/clk/SIMD)
+# SIMD cycles per wave64 VALU instruction (MI355X_MICROARCH.md, cdna_hip_programming.md:
+# v_fma_f32 2 on a SIMD-32; v_pk_*_f32 4, two f32 operations per lane at the same
+# 64 FLOP/clk/SIMD; transcendental 4; fp64 FMA/MUL/ADD 4 at 78.6 TF), checked
+# chip-wide by tools/micro/valu_cal.hip (profiles/r06_micro_valu_cal.json)
+VALU_CYC, PK_CYC, TRANS_CYC, F64_CYC = 2, 4, 4, 4
 CLOCK = 2.4e9                  # max shader clock
 TOL = 1e-5                     # north-star relative waveform tolerance
 SNR_TOL_DB = 2e-4              # per-cell SNR tolerance of the parity tests
@@ -655,60 +654,53 @@ def main():
         sys.exit("parity check failed: " + json.dumps(res["parity"]))
 
 
-def occupancy_probe():
-    """The r05 occupancy evidence (profiles/r05_occupancy_probe.json,
-    tools/occupancy_probe.sh): the r04 kernel reduced to OMLSA hop 128 with its
-    LDS cut to 35 KB (timing build, tools/probes/occupancy_probe4.patch) at 3
-    and at 4 waves/SIMD, and the full kernel with the split pass 2 (CSE_SPLIT_T)
-    at 3 and 4 (the 4-wave build spills 344 B/lane at 128 VGPRs)."""
-    path = os.path.join(REPO, "profiles", "r05_occupancy_probe.json")
+def valu_calibration():
+    """The chip-wide VALU rates the pricing rests on (tools/micro/valu_cal.hip,
+    HIP-event timed, profiles/r06_micro_valu_cal.json): TFLOP/s and SIMD cycles
+    per wave-instruction of dense independent streams at 8 and 3 waves/SIMD."""
+    path = os.path.join(REPO, "profiles", "r06_micro_valu_cal.json")
     if not os.path.exists(path):
         return None
-    b = json.load(open(path))["builds"]
-    out = {"source": "profiles/r05_occupancy_probe.json"}
-    for k in ("p3", "p4", "s3", "s4", "libcse"):
-        if k in b:
-            e = b[k]
-            out[k] = {"kernel_ms": round(e["kernel_ms_median"], 3), "vgprs_alloc": e["vgprs_alloc"],
-                      "lds_bytes": e["lds_bytes"], "scratch_bytes_per_lane": e["scratch_bytes_per_lane"],
-                      "mean_waves_per_simd": round(e["mean_waves_per_simd"], 2),
-                      "share_wait_inst_any": round(e["share_wait_inst_any"], 3),
-                      "share_wait_any": round(e["share_wait_any"], 3),
-                      "share_active_inst_any": round(e["share_active_inst_any"], 3)}
-    if "p3" in b and "p4" in b:
-        out["p4_over_p3_time"] = b["p4"]["kernel_ms_median"] / b["p3"]["kernel_ms_median"]
+    rows = json.load(open(path))["rows"]
+    out = {"source": "profiles/r06_micro_valu_cal.json (tools/micro/valu_cal.hip)"}
+    for r in rows:
+        if r["waves_per_simd"] in (3, 8):
+            out[f'{r["op"]}@{r["waves_per_simd"]}w'] = {"TFLOPs": round(r["tflops"], 2),
+                                                          "cycles_per_wave_inst": round(r["cycles_per_wave_inst"], 3)}
     return out
 
 
 def roofline_block(n_fft, units, kern_ms):
-    """The enhance kernel against the resource it spends: VALU issue.
+    """The enhance kernel against the resource it spends: VALU lane-op throughput.
 
     The product binary's own instruction counts (PMC of this launch size and
     n_fft, committed under profiles/ and matched to this build by a digest of
-    the kernel sources and flags): `achieved` = its issue cycles (wave64 f32
-    VALU 2 cycles on a SIMD-32, a packed v_pk_* instruction too: it issues at
-    the scalar rate, tools/micro/valu_peak.hip; transcendental 4) / the live
-    HIP-event kernel time; `peak` = 1024 SIMDs x 2.4 GHz.  Beside it:
-      dense_at_occupancy  the same counts priced at what a dependency-free
-                          VALU stream sustains at the kernel's own waves per
-                          SIMD (tools/micro/valu_peak.hip): how much of the
-                          issue shortfall occupancy alone explains;
-      fp32_flops          SQ_INSTS_VALU_FLOPS_FP32 (per wave-instruction,
-                          weighted by the FLOPs of each lane: x 64) against the
-                          157.3 TF FP32 vector peak;
-      traffic             the measured HBM bytes (PMC) and SURVEY 8(d)'s
-                          nominal 12 B/bin (read P, read N, write G) as a byte
-                          count only: the fused kernel never writes G and reads
-                          the shared rows once per 16-cell workgroup, so those
-                          bytes are not moved and are not a bandwidth."""
+    the kernel sources and flags), each priced at what it holds a SIMD-32
+    (VALU_CYC, PK_CYC, TRANS_CYC, F64_CYC: f32 VALU 2 cycles, packed v_pk_*_f32
+    4 since it carries two f32 operations per lane at the same 64 FLOP/clk/SIMD
+    peak, transcendental 4, fp64 4), over the live HIP-event kernel time:
+    `achieved` = those SIMD cycles per second, `peak` = 1024 SIMDs x 2.4 GHz.
+    The packed count is measured (tools/pmc_summary.py: the F32 class counters
+    of the scalar build CSE_PK=0 minus the product's, checked by the FLOP
+    counter).  Beside it:
+      fp32_flops   SQ_INSTS_VALU_FLOPS_FP32 (per wave-instruction, weighted by
+                   the FLOPs of each lane: x 64) against the 157.3 TF FP32 peak;
+      calibration  the chip-wide micro-benchmark of the per-instruction prices;
+      traffic      the measured HBM bytes (PMC) and SURVEY 8(d)'s nominal
+                   12 B/bin (read P, read N, write G) as a byte count only: the
+                   fused kernel never writes G and reads the shared rows once per
+                   16-cell workgroup, so those bytes are not moved and are not
+                   a bandwidth."""
     bytes_per_unit = 12 * (n_fft // 2 + 1)
     ks = kern_ms / 1e3
     nominal = units * bytes_per_unit
-    roof = {"bound": ("valu issue at the kernel's occupancy (3 waves/SIMD): see dense_at_occupancy, "
-                      "lds_array_busy and occupancy_probe (a 4th wave buys 3.9 %)"),
+    roof = {"bound": "valu",
+            "bound_note": ("VALU lane-op throughput: every VALU instruction of the launch priced at the "
+                           "SIMD cycles it takes (f32 2, packed f32 4, transcendental 4, f64 4 per wave64 "
+                           "instruction on a SIMD-32); HBM traffic is 2 % of peak"),
             "achieved": None,
             "peak": SIMDS * CLOCK / 1e9,
-            "unit": "G SIMD issue-cycles/s (1024 SIMDs)", "frac": None, "traffic": None,
+            "unit": "G SIMD VALU cycles/s (1024 SIMDs x 2.4 GHz)", "frac": None, "traffic": None,
             "kernel": f"cse::enhance_kernel<{n_fft}>", "kernel_ms": kern_ms,
             "units_per_launch": units,
             "nominal_unfused_bytes_per_unit": bytes_per_unit,
@@ -718,9 +710,8 @@ def roofline_block(n_fft, units, kern_ms):
                                      "bytes, so no bandwidth is derived from them"),
             "pmc_traffic_over_nominal": None,
             "hbm_measured_GBps": None, "hbm_measured_frac": None,
-            "kernel_src_sha": kernel_src_sha()}
-    if n_fft == 512:
-        roof["occupancy_probe"] = occupancy_probe()
+            "kernel_src_sha": kernel_src_sha(),
+            "calibration": valu_calibration()}
     pmc = load_pmc(units, n_fft)
     if not pmc:
         roof["note"] = "no committed PMC profile for this launch size: VALU figures absent"
@@ -738,25 +729,25 @@ def roofline_block(n_fft, units, kern_ms):
         roof["hbm_measured_frac"] = tb / ks / HBM_PEAK
         roof["pmc_traffic_over_nominal"] = tb / nominal
     vi, tr = pmc.get("sq_insts_valu"), pmc.get("sq_insts_valu_trans")
-    if vi and tr is not None:
-        need = VALU_CYC * (vi - tr) + TRANS_CYC * tr
+    pk, f64 = pmc.get("packed_insts"), pmc.get("sq_insts_valu_f64") or 0.0
+    if vi and tr is not None and pk is not None:
+        need = VALU_CYC * (vi - tr - pk - f64) + PK_CYC * pk + TRANS_CYC * tr + F64_CYC * f64
         roof["achieved"] = need / ks / 1e9
         roof["frac"] = need / ks / (SIMDS * CLOCK)
-        roof["issue_cycles_per_launch"] = need
-        roof["cycles_per"] = ("wave64 VALU 2 (packed v_pk_* too), transcendental 4 per SIMD; "
-                              "this binary's own SQ_INSTS_VALU / _TRANS_F32")
+        roof["valu_cycles_per_launch"] = need
+        roof["valu_insts"] = vi
+        roof["packed_insts"] = pk
+        roof["trans_insts"] = tr
+        roof["f64_insts"] = f64
+        roof["cycles_per"] = {"f32_valu": VALU_CYC, "packed_f32": PK_CYC, "transcendental": TRANS_CYC,
+                              "f64": F64_CYC}
+        if pmc.get("packed"):
+            roof["packed_source"] = {k: pmc["packed"].get(k) for k in ("add", "mul", "fma", "flop_check",
+                                                                        "valu_difference")}
         clk = pmc.get("clock_ghz_profiled")
         if clk:
             roof["clock_ghz_profiled"] = clk
             roof["frac_at_held_clock"] = need / ks / (SIMDS * clk * 1e9)
-        w = pmc.get("waves_per_simd")
-        if w in DENSE_CYC and clk:
-            fma, _, exp = DENSE_CYC[w]
-            dense = fma * (vi - tr) + exp * tr
-            roof["dense_at_occupancy"] = {
-                "waves_per_simd": w, "cycles_per_valu": fma, "cycles_per_trans": exp,
-                "frac": dense / (SIMDS * clk * 1e9 * ks),
-                "source": "tools/micro/valu_peak.hip (profiles/r05_micro_valu_peak.txt)"}
         fl = pmc.get("sq_insts_valu_flops_fp32")
         if fl:
             roof["fp32_flops"] = {"achieved_TFLOPs": fl * 64 / ks / 1e12,
@@ -769,6 +760,8 @@ def roofline_block(n_fft, units, kern_ms):
                   "lds_array_busy", "lds_conflict_cycles_per_lds_inst", "vgprs", "waves_per_simd"):
             if pmc.get(k) is not None:
                 roof[k] = pmc[k]
+    elif vi:
+        roof["note"] = "the committed PMC profile has no packed-instruction count: VALU figures omitted"
     return roof
 
 

@@ -25,32 +25,8 @@
 #include "cse_common.hpp"
 #include "cse_special.hpp"
 
-#ifndef CSE_JIT_TABLES
-#define CSE_JIT_TABLES 0  // experiment: table reads just before use (register pressure)
-#endif
 #ifndef CSE_PK
 #define CSE_PK 1  // n_fft 512: packed f32 (v_pk_*) gain pairs, packing and DFTs
-#endif
-// row loads through buffer resources, branch-free (r05, 13 pairs, three
-// alternating rounds: 512 22.50 / 22.51 / 22.51 -> 22.06 / 22.09 / 22.10 ms;
-// 1024 55.5 / 55.3 against 54.9 / 55.3 ms, so 1024 keeps the masked loads)
-#ifndef CSE_ROWS_BUF
-#define CSE_ROWS_BUF 1
-#endif
-#ifndef CSE_ROWS_BUF_1024
-#define CSE_ROWS_BUF_1024 0
-#endif
-#ifndef CSE_PK_1024
-#define CSE_PK_1024 0  // the same at n_fft 1024 (r04: 53.3 against 52.8 ms at 13 pairs, so off)
-#endif
-#ifndef CSE_ROT_TABLE_1024
-#define CSE_ROT_TABLE_1024 0  // 1024: packing rotors as base x W32^j (the table measured slower)
-#endif
-#ifndef CSE_T_ROWS
-#define CSE_T_ROWS 1  // n_fft 512 packed pass 2: lanes write block rows, read block columns
-#endif
-#ifndef CSE_SPLIT_T
-#define CSE_SPLIT_T 0  // n_fft 512 sweep kernel: pass 2 through a half block (see WG::SPLIT)
 #endif
 
 namespace cse {
@@ -278,16 +254,9 @@ struct WG {
     // (gamma, d) / (N, P) float2 [B] at 512); A (float [B], 512: MMSE's
     // c/(gamma + 1e-12), SS's 1/|Y|); clean (float [HMAX])
     static constexpr bool R2 = (NFFT == 512);
-    // packed pairs (CSE_PK): the rows in mirror-pair order, 16-B records
-    static constexpr bool PK = R2 ? CSE_PK : CSE_PK_1024;
-    // Pass 2 through half a transpose block (n_fft 512 sweep kernel): rows
-    // b < 8 of the 16 x 16 block, then rows b >= 8, each lane reading half a
-    // row; lanes i and i ^ 8 (one DPP row of the cell) finish the first
-    // radix-2 step of the DFT16 over the columns with a row_ror:8 exchange and
-    // own the even / odd outputs of rows i & 7 and (i & 7) + 8 (two DFT8s).
-    // The per-cell region shrinks from 2,176 to the exchange slots' 1,152 B
-    // (16 cells: 34.8 -> 18.4 KB of LDS), with no register more in flight.
-    static constexpr bool SPLIT = R2 && PK && CSE_SPLIT_T && !OUT;
+    // packed pairs (CSE_PK, n_fft 512; packing the 1024 kernel measured slower,
+    // DESIGN.md §3.1): the rows in mirror-pair order, 16-B records
+    static constexpr bool PK = R2 && CSE_PK;
     // per-cell LDS region: the mirror-exchange slots (9 complex per lane,
     // stride 72 B: the 16 lanes of a ds_write_b64 group hit disjoint banks)
     // aliased with the transpose block (16 rows x TS = L + 1 complex).  Its
@@ -299,9 +268,7 @@ struct WG {
     static constexpr int TB = 16 * TS * 8;
     static constexpr int CREG_RAW = XB > TB ? XB : TB;
     static constexpr int CREG_U = (CREG_RAW + 127) / 128;
-    static constexpr int CREG = SPLIT ? XB : (CREG_U + (CREG_U % 2 ? 0 : 1)) * 128;
-    static constexpr int TS2 = 17;  // SPLIT: row stride (complex) of the half block
-    static_assert(!SPLIT || (8 * TS2 * 8 <= XB && XB % 256 == 128), "half block in the exchange slots");
+    static constexpr int CREG = (CREG_U + (CREG_U % 2 ? 0 : 1)) * 128;
     static constexpr int YROW = ((G::B * 8 + 15) / 16) * 16;      // bytes of one Y row
     static constexpr int GROW = ((G::B * (R2 ? 8 : 4) + 15) / 16) * 16;
     static constexpr int AROW = R2 ? ((G::B * 4 + 15) / 16) * 16 : 0;
@@ -331,7 +298,9 @@ struct WG {
     // packing rotors e^{2πi (i + L j)/NFFT}: a row of the 8 (j < 8) per lane,
     // stride 80 B (20 dwords: the ds_read_b128 of a 16-lane group hit
     // disjoint banks), 4 ds_read_b128 per frame instead of 7 complex products
-    static constexpr bool ROT_TABLE = R2 || CSE_ROT_TABLE_1024;
+    // (n_fft 1024: base x W32^j; its 2.5-KB table pushed the workgroup past the
+    // LDS budget, +11 %)
+    static constexpr bool ROT_TABLE = R2;
     static constexpr int ROTSTR = 80;
     static constexpr int OFF_LC = OFF_TW + (ROTOR_TW ? G::L * 48 : TWL * 144);
     static constexpr int OFF_CP = OFF_LC + G::L * (ROT_TABLE ? ROTSTR : 8);  // CellParam[CPWG]
@@ -342,11 +311,7 @@ struct WG {
     static constexpr int WSLOTS = HALF_TABLES ? 16 : 32;
     static constexpr int WSTR = HALF_TABLES ? 20 : 36;
     static constexpr int OFF_WIN = OFF_CP + CPWG * 32;
-    // SPLIT: the odd-output twiddles W16^c (c = 1..7) of lanes i >= 8, (1, 0)
-    // for lanes i < 8 (branch-free, VGPR operands: as SGPR pairs of constants
-    // the twiddles spilled 90 SGPRs), a row of 8 complex per lane, stride 80 B
-    static constexpr int OFF_T2 = OFF_WIN + G::L * WSTR * 4;
-    static constexpr int BYTES = OFF_T2 + (SPLIT ? G::L * 80 : 0);
+    static constexpr int BYTES = OFF_WIN + G::L * WSTR * 4;
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
@@ -463,14 +428,10 @@ __device__ __forceinline__ float gain_bin(float2& y, RowV rv, float& rr, float a
 // (OMLSA: times log2 e), d = (d_k, d_{M-k}), a = MMSE's (c/(gamma + 1e-12))
 // pair.  Returns the pair's gains; rr is the pair's decision-directed state.
 // ---------------------------------------------------------------------------
-#ifndef CSE_PK_HORNER
-#define CSE_PK_HORNER 1  // r04: scalar chains 24.1 against 23.1 ms at 13 pairs (512)
-#endif
-// a polynomial on both lanes: packed (coefficients from SGPR pairs) or as two
-// scalar chains (coefficients as instruction literals, no SGPRs)
+// a polynomial on both lanes, packed (coefficients from SGPR pairs; as two
+// scalar chains with literal coefficients, r04: 24.1 against 23.1 ms at 13 pairs)
 template <int N>
 __device__ __forceinline__ f2 horner2(const float (&c)[N], f2 t) {
-    if (!CSE_PK_HORNER) return f2{horner(c, t.x), horner(c, t.y)};
     f2 acc = pdup(c[N - 1]);
 #pragma unroll
     for (int k = N - 2; k >= 0; --k) acc = pfma(acc, t, pdup(c[k]));
@@ -482,25 +443,17 @@ __device__ __forceinline__ f2 pmed3(f2 x, float lo, float hi) {
 }
 __device__ __forceinline__ f2 pmax(f2 x, float lo) { return f2{fmaxf(x.x, lo), fmaxf(x.y, lo)}; }
 
-template <int NFFT, int ALGO>
+template <int ALGO>
 __device__ __forceinline__ f2 gain_pair(f2 gam, f2 d, f2 a, f2& rr, float alpha_t, const CellParam& cp) {
-    constexpr bool R2 = (NFFT == 512);
-    // dd = (1 - alpha_t) max(gamma - 1, 0): the stager's d row at 512; at 1024
-    // max((1 - alpha_t) gamma - (1 - alpha_t), 0) (OMLSA's gamma carries log2 e)
-    const float a_d = 1.0f - alpha_t;
-    f2 dd;
-    if constexpr (R2) {
-        dd = d * pdup(a_d);
-    } else {
-        dd = pmax(pfma(gam, pdup(ALGO == CSE_ALGO_OMLSA ? a_d * kLn2 : a_d), pdup(-a_d)), 0.0f);
-    }
+    // dd = (1 - alpha_t) max(gamma - 1, 0) from the stager's d row
+    const f2 dd = d * pdup(1.0f - alpha_t);
     if (ALGO == CSE_ALGO_WIENER) {
         const f2 xi = pmax(pfma(pdup(alpha_t), rr, dd), 1e-10f);
         const f2 g = pmed3(xi * prcp(xi + 1.0f), cp.p1, 1.0f);
         rr = (g * g) * gam;
         return g;
     } else if (ALGO == CSE_ALGO_MMSE) {
-        const f2 cig = R2 ? a : prcp(gam + 1e-12f) * pdup(0.88622692545275801f);
+        const f2 cig = a;  // the stager's (sqrt(pi)/2)/(gamma + 1e-12) row
         const f2 xi = pmax(pfma(pdup(alpha_t), rr, dd), cp.p1);
         const f2 v = pmed3((xi * gam) * prcp(xi + 1.0f), 1e-12f, 80.0f);
         const f2 sv = f2{__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
@@ -545,9 +498,8 @@ __device__ __forceinline__ f2 gain_pair(f2 gam, f2 d, f2 a, f2& rr, float alpha_
 //   Z'[k] = S + i P,  Z'[M - k] = conj(S) + i conj(P)
 // (8 packed instructions per pair).  z[j] keeps Z'[k]; xw[j] goes to the
 // mirror lane.  Bin M/2 (the 17th item) stays scalar (gain_bin).  Rows: Y
-// records (Y_p, Y_{M-p}) (16 B); at 512 (g_p, g_{M-p}, d_p, d_{M-p}) (16 B) and
-// MMSE's / SS's a pairs (8 B), at 1024 (g_p, g_{M-p}) (8 B).  Packing rotors:
-// the lane's table row (512) or base x W32^j (1024).
+// records (Y_p, Y_{M-p}) (16 B), (g_p, g_{M-p}, d_p, d_{M-p}) (16 B) and
+// MMSE's / SS's a pairs (8 B).  Packing rotors: the lane's table row.
 template <int NFFT, int ALGO, bool OUT>
 __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
                                              const void* __restrict__ growv,
@@ -555,24 +507,19 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
                                              f2* __restrict__ xw, f2 (&rr)[8], float& rrm,
                                              float alpha_t, const CellParam& cpar,
                                              const float4* __restrict__ rot4,
-                                             const cf* __restrict__ base_p,
                                              float* __restrict__ gout_row, int i) {
+    // (instantiated for 1024 too, where W::PK is false and the frame never calls it)
     constexpr int L = Geo<NFFT>::L, M = Geo<NFFT>::M;
-    constexpr bool R2 = (NFFT == 512);
-    constexpr bool WANT_A = R2 && (ALGO == CSE_ALGO_MMSE || (ALGO == CSE_ALGO_SS && OUT));
+    constexpr bool WANT_A = ALGO == CSE_ALGO_MMSE || (ALGO == CSE_ALGO_SS && OUT);
     const float4* y4 = y4row + i;
-    const float4* g4 = (const float4*)growv + i;  // 512
-    const float2* g2 = (const float2*)growv + i;  // 1024
+    const float4* g4 = (const float4*)growv + i;
     const float2* a2 = a2row + i;
-    // (gamma pair, d pair) of a record: d unused at 1024
-    auto ldg = [&](int k) {
-        if constexpr (R2) return g4[k];
-        const float2 v = g2[k];
-        return make_float4(v.x, v.y, 0.0f, 0.0f);
-    };
+    // the records through a by-value copy: reading g4[k] in place lets the
+    // compiler turn bin M/2's two 4-byte reads into a ds_read_b128 and
+    // reschedule the frame; this form keeps r05's measured instruction stream
+    auto ldg = [&](int k) -> float4 { const float4 v = g4[k]; return v; };
     float4 yc = y4[0], gc = ldg(0);
     float2 ac = WANT_A ? a2[0] : make_float2(0.0f, 0.0f);
-    const cf base = R2 ? cmk(1.0f, 0.0f) : *base_p;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         // next pair's rows (j = 7: bin M/2, the record of pair M/2)
@@ -589,11 +536,9 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
             const float s1 = gain_bin<NFFT, ALGO>(y1, RowV{gc.y, gc.w, ac.y}, dummy, alpha_t, cpar, g1);
             g = f2{g0, g1};
             s = f2{s0, s1};
-            ya = f2{y0.x, y0.y};  // 1024: the rescaled phasor source where Y is tiny
-            yb = f2{y1.x, y1.y};
         } else {
-            g = gain_pair<NFFT, ALGO>(f2{gc.x, gc.y}, f2{gc.z, gc.w}, f2{ac.x, ac.y}, rr[j],
-                                      alpha_t, cpar);
+            g = gain_pair<ALGO>(f2{gc.x, gc.y}, f2{gc.z, gc.w}, f2{ac.x, ac.y}, rr[j],
+                                 alpha_t, cpar);
             s = g;
         }
         if (OUT && gout_row) {
@@ -606,15 +551,8 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
         }
         const f2 xk = ya * s.xx;
         const f2 S = p_fma_conj_hi(yb, s, xk), D = p_fms_conj_hi(yb, s, xk);
-        f2 w;
-        if constexpr (R2) {
-            const float4 q4 = rot4[j >> 1];  // two packing rotors
-            w = (j & 1) ? f2{q4.z, q4.w} : f2{q4.x, q4.y};
-        } else {
-            // base x W32^j in scalar form (instruction literals, no SGPR pairs)
-            const cf wj = (j == 0) ? base : cmul(base, cmk(Rot32::c[j], Rot32::s[j]));
-            w = f2{wj.x, wj.y};
-        }
+        const float4 q4 = rot4[j >> 1];  // two packing rotors
+        const f2 w = (j & 1) ? f2{q4.z, q4.w} : f2{q4.x, q4.y};
         const f2 P = p_cmul(D, w);
         z[j] = p_addi(S, P);                      // Z'[k] = S + i P
         xw[j] = p_conj_addi(S, P);                // Z'[M - k] = conj(S) + i conj(P)
@@ -754,31 +692,15 @@ __device__ __forceinline__ void gain_pack(const float2* __restrict__ yrow,
 }
 
 // Position inside a frame (relative to the lane's first sample) of the lane's
-// output slot q: the pass-2 DFT16 gives lane b2 the samples 2 b2 + 32 p + e
-// (slot q = 2 p + e); the split pass 2 gives lane i = 8 h + l the samples
-// 2 l + 32 h + 16 r + 64 s + e of rows l + 8 r (slot q = 4 s + 2 r + e).  Either
-// way slot q + F lies HOP samples after slot q.
-template <bool SPLIT, int SP>
+// output slot q: the pass-2 DFT16 gives lane b2 the samples 2 b2 + SP p + e
+// (slot q = 2 p + e), so slot q + F lies HOP samples after slot q.
+template <int SP>
 __device__ __forceinline__ constexpr int slot_pos(int q) {
-    return SPLIT ? 64 * (q >> 2) + 16 * ((q >> 1) & 1) + (q & 1) : SP * (q >> 1) + (q & 1);
+    return SP * (q >> 1) + (q & 1);
 }
 
-// The eight (hop, algorithm) bodies as separate functions (CSE_RUNWG_NOINLINE,
-// the n_fft 512 unit at 4 waves/SIMD): inlined into one kernel, the compiler
-// hoisted every body's constants to the entry and the union spilled 160
-// VGPRs and 70 SGPRs at the 128-VGPR cap; as callees each body is allocated
-// on its own (one call per workgroup)
-#ifndef CSE_RUNWG_NOINLINE
-#define CSE_RUNWG_NOINLINE 0
-#endif
-#if CSE_RUNWG_NOINLINE
-#define CSE_RUNWG_ATTR __noinline__
-#else
-#define CSE_RUNWG_ATTR __forceinline__
-#endif
-
 template <int NFFT, int HOP, int ALGO, bool OUT>
-__device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, int n_cells_wg,
+__device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, int n_cells_wg,
                                        unsigned char* smem) {
     using G = Geo<NFFT>;
     using W = WG<NFFT, OUT>;
@@ -860,31 +782,19 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
     for (int e = tid; e < L * 32; e += W::THREADS) {
         const int ii = e / 32, q = e % 32;
         const int bb = (L == 16) ? ii : (ii & 15), hh = (L == 16) ? 0 : (ii >> 4);
-        const int n = (W::SPLIT ? 2 * (ii & 7) + 32 * (ii >> 3) : 2 * bb + 32 * hh) +
-                      slot_pos<W::SPLIT, SP>(q);
+        const int n = 2 * bb + 32 * hh + slot_pos<SP>(q);
         const double w = 0.5 - 0.5 * cospi(2.0 * (double)n / (double)NFFT);
         double S = 0.0;
         for (int m = n % HOP; m < NFFT; m += HOP) {
             const double wm = 0.5 - 0.5 * cospi(2.0 * (double)m / (double)NFFT);
             S += wm * wm;
         }
-        // SPLIT: lanes i >= 8 hold the negated odd outputs (see pass 2); their
-        // window entries carry the sign back
-        const double wn = (W::SPLIT && (ii & 8)) ? -w : w;
-        if (q < W::WSLOTS) ((float*)(smem + W::OFF_WIN))[ii * W::WSTR + q] = (float)(wn / (NFFT * S));
+        if (q < W::WSLOTS) ((float*)(smem + W::OFF_WIN))[ii * W::WSTR + q] = (float)(w / (NFFT * S));
         if (W::ROT_TABLE ? q < 8 : q == 0) {
             double sn, cn;
             sincospi(2.0 * (double)(ii + L * q) / (double)NFFT, &sn, &cn);
             ((cf*)(smem + W::OFF_LC + (W::ROT_TABLE ? W::ROTSTR : 8) * ii))[q] =
                 cmk((float)cn, (float)sn);
-        }
-    }
-    if constexpr (W::SPLIT) {
-        for (int e = tid; e < L * 8; e += W::THREADS) {
-            const int ii = e >> 3, c = e & 7;
-            double sn = 0.0, cn = 1.0;
-            if (ii & 8) sincospi((double)c / 8.0, &sn, &cn);  // W16^c = e^{2πi c/16}
-            ((cf*)(smem + W::OFF_T2 + 80 * ii))[c] = cmk((float)cn, (float)sn);
         }
     }
     for (int c = tid; c < W::CPWG; c += W::THREADS) {
@@ -922,7 +832,11 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
     // clean samples stay f64 in flight: converting at load time made the
     // compiler wait (vmcnt(0)) for every row load right after issuing them
     double pc[W::CPT];
-    constexpr bool ROWS_BUF = NFFT == 512 ? CSE_ROWS_BUF : CSE_ROWS_BUF_1024;
+    // n_fft 512: the row loads through buffer resources, branch-free (r05, 13
+    // pairs, three alternating rounds: 22.50 / 22.51 / 22.51 -> 22.06 / 22.09 /
+    // 22.10 ms; at 1024 55.5 / 55.3 against 54.9 / 55.3 ms, so 1024 keeps the
+    // masked loads)
+    constexpr bool ROWS_BUF = NFFT == 512;
     // ROWS_BUF: the row loads through buffer resources (r05): an index past a
     // row's end returns 0 instead of taking a per-lane branch.  Y: the
     // workgroup's nf frames; N: the same for a time-varying row, the static row
@@ -1016,8 +930,8 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                     if (!W::R2) {
                         const float gam = fmaxf(P * pn[u], EPS);
                         const float gv = (ALGO == CSE_ALGO_SS) ? pn[u] : (ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam);
-                        yrow[W::PK ? 2 * pp + hh : k] = y;  // pair order: 8-B gamma records
-                        grow[W::PK ? 2 * pp + hh : k] = gv;
+                        yrow[k] = y;
+                        grow[k] = gv;
                     } else if (ALGO == CSE_ALGO_SS) {
                         // phasor y/|y| of the y rescaled by 2^64 below 2^-50
                         // (v_rsq flushes denormals); (1, 0) where y = 0
@@ -1065,7 +979,7 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
     const int b2 = (L == 16) ? i : (i & 15);
     const int h2 = (L == 16) ? 0 : (i >> 4);
     // lane's first sample offset inside a frame
-    const int off = W::SPLIT ? 2 * (i & 7) + 32 * (i >> 3) : 2 * b2 + 32 * h2;
+    const int off = 2 * b2 + 32 * h2;
 
     float rr[17];  // prev_gain**2 * prev_gamma per bin (read from frame 1 on)
 #pragma unroll
@@ -1121,7 +1035,6 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                                               (const float2*)(smem + ab), z, (f2*)(smem + creg + 72 * i),
                                               rr2, rrm, alpha_t, cpar,
                                               (const float4*)(smem + W::OFF_LC + W::ROTSTR * i),
-                                              (const cf*)(smem + W::OFF_LC + 8 * i),
                                               (OUT && gout) ? gout + t * B : nullptr, i);
             }
             __builtin_amdgcn_s_setprio(0);
@@ -1130,45 +1043,19 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
             {
                 const int partner = (L - i) & (L - 1);
                 const int xo = creg + 72 * partner + (i == 0 ? 8 : 0);
-                if constexpr (CSE_T_ROWS && L == 16) {
-                    // entries 7, 5, 3, 1 and 6, 4, 2, 0 from two unrelated bases:
-                    // 8 ds_read_b64 (2 LDS cycles each), not 4 ds_read2_b64 (8)
-                    const f2* xe = (const f2*)(smem + opaque_off(xo));
-                    const f2* xd = (const f2*)(smem + opaque_off(xo + 8));
+                // entries 7, 5, 3, 1 and 6, 4, 2, 0 from two unrelated bases:
+                // 8 ds_read_b64 (2 LDS cycles each), not 4 ds_read2_b64 (8)
+                const f2* xe = (const f2*)(smem + opaque_off(xo));
+                const f2* xd = (const f2*)(smem + opaque_off(xo + 8));
 #pragma unroll
-                    for (int s = 8; s < 16; ++s) z[s] = ((15 - s) & 1) ? xd[14 - s] : xe[15 - s];
-                } else {
-                    const f2* xr = (const f2*)(smem + xo);
-#pragma unroll
-                    for (int s = 8; s < 16; ++s) z[s] = xr[15 - s];
-                }
+                for (int s = 8; s < 16; ++s) z[s] = ((15 - s) & 1) ? xd[14 - s] : xe[15 - s];
             }
             CSE_MARK("rows");
             store_rows(t + 1);
             load_rows(t + 2);
             CSE_MARK("pass1");
-            if constexpr (W::ROTOR_TW) {  // see the scalar branch
-                const float4* q4 = (const float4*)(smem + W::OFF_TW + 48 * i);
-                const float4 qa = q4[0], qb = q4[1], qc = q4[2];
-                idft16_pk(z);
-                const f2 lo[4] = {f2{1.0f, 0.0f}, f2{qa.x, qa.y}, f2{qa.z, qa.w}, f2{qb.x, qb.y}};
-                const f2 hi[4] = {f2{1.0f, 0.0f}, f2{qb.z, qb.w}, f2{qc.x, qc.y}, f2{qc.z, qc.w}};
-#pragma unroll
-                for (int b = 1; b < 16; ++b) {
-                    const f2 tb = (b & 3) == 0 ? hi[b >> 2] : (b < 4 ? lo[b] : p_cmul(lo[b & 3], hi[b >> 2]));
-                    z[b] = p_cmul(z[b], tb);
-                }
-            } else {
+            {  // pass-1 twiddles from the lane's table row (8 ds_read_b128), issued ahead of the DFT
                 const float4* twr = (const float4*)(smem + W::OFF_TW + 144 * i);
-#if CSE_JIT_TABLES  // each twiddle pair read right before its products
-                idft16_pk(z);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const float4 q4 = twr[k];
-                    z[2 * k + 1] = p_cmul(z[2 * k + 1], f2{q4.x, q4.y});
-                    if (k < 7) z[2 * k + 2] = p_cmul(z[2 * k + 2], f2{q4.z, q4.w});
-                }
-#else
                 float4 t4[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) t4[k] = twr[k];
@@ -1178,115 +1065,30 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                     const float4 q4 = t4[(b - 1) >> 1];
                     z[b] = p_cmul(z[b], ((b - 1) & 1) ? f2{q4.z, q4.w} : f2{q4.x, q4.y});
                 }
-#endif
             }
             CSE_MARK("pass2");
             f2 v[16];
-            if constexpr (W::SPLIT) {
-                // x[b + 16 r'] = sum_i V[b][i] W16^{i r'} with i = c + 8 h:
-                //   even r' = 2s: DFT8_c of V[b][c] + V[b][c + 8]
-                //   odd r' = 2s + 1: DFT8_c of (V[b][c] - V[b][c + 8]) W16^c.
-                // Lane i = 8 hp + l reads columns 8 hp + c of row l (round 1) and
-                // of row l + 8 (round 2); u += sg dpp(u) with the partner lane
-                // i ^ 8 (row_ror:8 inside the cell's DPP row) gives hp = 0 the
-                // sums and hp = 1 the negated differences (the window entries of
-                // lanes hp = 1 are negated to match).
-                constexpr int TS2 = W::TS2;
-                const int l = i & 7, hp = i >> 3;
-                const float sg = hp ? -1.0f : 1.0f;
-                f2* blk_w = (f2*)(smem + creg) + i;                        // + TS2 b
-                const f2* blk_r = (const f2*)(smem + creg) + TS2 * l + 8 * hp;  // + c
-                auto radix2 = [&](f2 (&u)[8]) {
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) {
-                        // v_mov_b32_dpp row_ror:8 (0x128): the value of lane i ^ 8
-                        auto ror8 = [](float x) {
-                            return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                                0, __builtin_bit_cast(int, x), 0x128, 0xf, 0xf, false));
-                        };
-                        const f2 q = f2{ror8(u[c].x), ror8(u[c].y)};
-                        u[c] = pfma(q, pdup(sg), u[c]);
-                    }
-                };
-                f2 u0[8], u1[8];
-                wave_sync();
-#pragma unroll
-                for (int b = 0; b < 8; ++b) blk_w[TS2 * b] = z[b];
-                wave_sync();
-#pragma unroll
-                for (int c = 0; c < 8; ++c) u0[c] = blk_r[c];
-                wave_sync();  // round 1's reads are issued before round 2 overwrites
-#pragma unroll
-                for (int b = 0; b < 8; ++b) blk_w[TS2 * b] = z[8 + b];
-                radix2(u0);
-                wave_sync();
-#pragma unroll
-                for (int c = 0; c < 8; ++c) u1[c] = blk_r[c];
-                radix2(u1);
-                {  // the odd outputs' twiddles W16^c (lanes hp = 0: (1, 0))
-                    const float4* t4 = (const float4*)(smem + W::OFF_T2 + 80 * i);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const float4 q4 = t4[k];  // entries 2k, 2k + 1 (entry 0 unused)
-                        if (k > 0) {
-                            u0[2 * k] = p_cmul(u0[2 * k], f2{q4.x, q4.y});
-                            u1[2 * k] = p_cmul(u1[2 * k], f2{q4.x, q4.y});
-                        }
-                        u0[2 * k + 1] = p_cmul(u0[2 * k + 1], f2{q4.z, q4.w});
-                        u1[2 * k + 1] = p_cmul(u1[2 * k + 1], f2{q4.z, q4.w});
-                    }
-                }
-                idft8_pk(u0);
-                idft8_pk(u1);
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    v[2 * q] = u0[q];
-                    v[2 * q + 1] = u1[q];
-                }
-            } else {
+            {
+                // lane i writes row i of the block (z[b] at column b), lane b2
+                // reads column b2: 16 ds_read_b64 at the row stride (the
+                // row-wise read merged into 8 ds_read2_b64, 8 LDS cycles per
+                // pair against 2 + 2); the even and odd columns' writes from
+                // unrelated bases stay ds_write_b64
                 constexpr int TS = W::TS;
                 wave_sync();
-                if constexpr (CSE_T_ROWS && L == 16) {
-                    // lane i writes row i of the block (z[b] at column b), lane
-                    // b2 reads column b2: 16 ds_read_b64 at the row stride (the
-                    // row-wise read merged into 8 ds_read2_b64, 8 LDS cycles per
-                    // pair against 2 + 2); the even and odd columns' writes from
-                    // unrelated bases stay ds_write_b64
-                    f2* we = (f2*)(smem + opaque_off(creg + 8 * TS * i));
-                    f2* wd = (f2*)(smem + opaque_off(creg + 8 * TS * i + 8));
+                f2* we = (f2*)(smem + opaque_off(creg + 8 * TS * i));
+                f2* wd = (f2*)(smem + opaque_off(creg + 8 * TS * i + 8));
 #pragma unroll
-                    for (int b = 0; b < 16; b += 2) {
-                        we[b] = z[b];
-                        wd[b] = z[b + 1];
-                    }
-                    wave_sync();
-                    const f2* tc = (const f2*)(smem + creg + 8 * b2);
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) v[r] = tc[r * TS];
-                } else {
-                f2* tw_ = (f2*)(smem + creg + 8 * i);
-                const f2* tr = (const f2*)(smem + creg + 8 * TS * b2);
-#pragma unroll
-                for (int b = 0; b < 16; ++b) tw_[b * TS] = z[b];
+                for (int b = 0; b < 16; b += 2) {
+                    we[b] = z[b];
+                    wd[b] = z[b + 1];
+                }
                 wave_sync();
-                if constexpr (L == 32) {  // DFT32: radix-2 on the read side, see the scalar branch
-                    const float sg = h2 ? -1.0f : 1.0f;
+                const f2* tc = (const f2*)(smem + creg + 8 * b2);
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const f2 u = pfma(pdup(sg), tr[r + 16], tr[r]);
-                        // the rotor product in scalar form: its constants are
-                        // instruction literals (16 packed rotor pairs would take
-                        // 64 SGPRs, and the kernel spilled 192)
-                        const cf ur = cmul(cmk(u.x, u.y), cmk(Rot32::c[r], Rot32::s[r]));
-                        v[r] = h2 ? f2{ur.x, ur.y} : u;
-                    }
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) v[r] = tr[r];
-                }
-                }
-                idft16_pk(v);
+                for (int r = 0; r < 16; ++r) v[r] = tc[r * TS];
             }
+            idft16_pk(v);
             CSE_MARK("window");
 #pragma unroll
             for (int p = 0; p < 16; ++p) xp[p] = v[p];
@@ -1348,15 +1150,6 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                 // pass-1 twiddles e^{2πi i' b/M}, b = 1..15, of my column (per-lane
                 // row of 18 complex: 8 ds_read_b128), issued ahead of the DFT
                 const float4* twr = (const float4*)(smem + W::OFF_TW + 144 * i);
-#if CSE_JIT_TABLES
-                idft16(z);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const float4 q4 = twr[k];
-                    z[2 * k + 1] = cmul(z[2 * k + 1], cmk(q4.x, q4.y));
-                    if (k < 7) z[2 * k + 2] = cmul(z[2 * k + 2], cmk(q4.z, q4.w));
-                }
-#else
                 float4 t4[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) t4[k] = twr[k];
@@ -1367,7 +1160,6 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                     const cf t = ((b - 1) & 1) ? cmk(q4.z, q4.w) : cmk(q4.x, q4.y);
                     z[b] = cmul(z[b], t);
                 }
-#endif
                 }
             }
             CSE_MARK("pass2");
@@ -1481,14 +1273,14 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                 float2 cl2[F / 2];  // the clean samples of slots q, q + 1
 #pragma unroll
                 for (int k = 0; k < F / 2; ++k)
-                    cl2[k] = *(const float2*)(crow_t + slot_pos<W::SPLIT, SP>(2 * k));
+                    cl2[k] = *(const float2*)(crow_t + slot_pos<SP>(2 * k));
                 float pa = 0.0f, pb = 0.0f, ca = 0.0f, cb = 0.0f;
                 if constexpr (W::PK) {  // the two chains as one pair
                     f2 pp = f2{0.0f, 0.0f}, cc = f2{0.0f, 0.0f};
 #pragma unroll
                     for (int p = 0; p < F / 2; ++p) {
                         const f2 y = done2[p];
-                        const int n = slot_pos<W::SPLIT, SP>(2 * p);
+                        const int n = slot_pos<SP>(2 * p);
                         if (head && yout && o0 + n < out_len) yout[o0 + n] = y.x;
                         if (head && yout && o0 + n + 1 < out_len) yout[o0 + n + 1] = y.y;
                         const f2 d = f2{cl2[p].x, cl2[p].y} - pmed3(y, -1.0f, 1.0f);
@@ -1502,7 +1294,7 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
                 }
 #pragma unroll
                 for (int q = 0; q < (W::PK ? 0 : F); ++q) {
-                    const int n = slot_pos<W::SPLIT, SP>(q);
+                    const int n = slot_pos<SP>(q);
                     const float y = done[q];
                     if (head && yout && o0 + n < out_len) yout[o0 + n] = y;
                     // np.clip as one v_med3 (fminf(fmaxf()) of a value carried
@@ -1522,7 +1314,7 @@ __device__ CSE_RUNWG_ATTR void run_wg(const Args& a, const cse_cell_t* wcell, in
             } else {
 #pragma unroll
                 for (int q = 0; q < F; ++q) {
-                    const int n = slot_pos<W::SPLIT, SP>(q);  // + off: position inside frame t
+                    const int n = slot_pos<SP>(q);  // + off: position inside frame t
                     const int o = o0 + n;
                     float iv = 1.0f;
                     if (edge) {
@@ -1671,9 +1463,9 @@ extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells
     CSE_CHECK_ARG(len >= 1 && len < (1ll << 30) && n_cells >= 0,
                   "cse_enhance_cells: len=%lld n_cells=%lld", (long long)len, (long long)n_cells);
     // n_fft 512 reads its rows through buffer resources with 32-bit byte
-    // offsets (CSE_ROWS_BUF): the signal's spectrum rows at the smallest hop
+    // offsets (run_wg's ROWS_BUF): the signal's spectrum rows at the smallest hop
     // must stay below 2 GiB
-    CSE_CHECK_ARG(n_fft != 512 || !CSE_ROWS_BUF || (1 + len / 128) * 257 * 8 < (1ll << 31),
+    CSE_CHECK_ARG(n_fft != 512 || (1 + len / 128) * 257 * 8 < (1ll << 31),
                   "cse_enhance_cells: len=%lld too long for n_fft=512 (spectrum rows >= 2 GiB)",
                   (long long)len);
     if (n_cells == 0) return CSE_OK;

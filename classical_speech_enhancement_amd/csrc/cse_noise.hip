@@ -681,12 +681,14 @@ __global__ void invert_kernel(const float* __restrict__ N, int64_t n, double eps
 // frames, one block ahead, with no per-frame conditions: r03's form (a bounds
 // check per load and per store) compiled to a branch per access and a full
 // vmcnt(0) wait per block.
-// correctly rounded 1/x in f32 for positive normal x < 2^60: v_rcp_f32 and one
-// FMA Newton step; checked against IEEE 1.0f / x for every positive normal f32
-// in [2^-60, 2^61) (tools/micro/rcp_check.hip: 0 mismatches in 1.0e9), so it
-// equals the division it replaces (3 VALU for the ~10 of the division sequence)
+// correctly rounded 1/x in f32 for x in [2^-60, 2^60): v_rcp_f32 and one FMA
+// Newton step; checked against IEEE 1.0f / x for every f32 in [2^-60, 2^61)
+// (tools/micro/rcp_check.hip: 0 mismatches in 1.0e9), so it equals the division
+// it replaces there (3 VALU for the ~10 of the division sequence).  Outside
+// that range (cse_noise_finish takes any inv_eps > 0, subnormal ones
+// included, which v_rcp_f32 may flush) the division itself.
 __device__ __forceinline__ float rcp_rn(float x) {
-    if (x < 0x1p60f) {
+    if (x >= 0x1p-60f && x < 0x1p60f) {
         const float r = __builtin_amdgcn_rcpf(x);
         return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
     }
@@ -747,6 +749,11 @@ struct Workspace {
     int* sel;        // [n_sig][T]
     double* med;     // [n_sig][B]
     double* S;       // [n_sig][T][B]
+    // cse_noise_percentile_quad's energies [2 eps][n_sig][T] (f64) and
+    // selections [2 pct][2 eps][n_sig][T] (int): a region of its own (r06;
+    // r05 borrowed S, so a min-tracking call on another stream with the same
+    // workspace would have raced it)
+    double* Q;
 };
 
 static int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
@@ -765,6 +772,8 @@ static Workspace carve(void* ws, int64_t n_sig, int T, int B) {
     w.med = (double*)p;
     p += align256(n_sig * (int64_t)B * 8);
     w.S = (double*)p;
+    p += align256(n_sig * (int64_t)T * B * 8);
+    w.Q = (double*)p;
     return w;
 }
 
@@ -920,7 +929,8 @@ using namespace cse;
 
 extern "C" int64_t cse_noise_workspace_bytes(int64_t n_sig, int T, int B) {
     return align256(n_sig * (int64_t)T * 8) + align256(n_sig * (int64_t)T * 4) +
-           align256(n_sig * (int64_t)B * 8) + align256(n_sig * (int64_t)T * B * 8);
+           align256(n_sig * (int64_t)B * 8) + align256(n_sig * (int64_t)T * B * 8) +
+           align256(n_sig * (int64_t)T * 32);
 }
 
 extern "C" void cse_noise_default_params(cse_noise_params_t* prm) {
@@ -1058,9 +1068,9 @@ extern "C" int cse_noise_percentile_quad(const double* P, const double* med, int
         }
         return CSE_OK;
     }
-    // the min-tracking IIR buffer w.S (>= 32 n_sig T bytes for B >= 16) holds
-    // the two energy rows and the four selections
-    double* en = w.S;                         // [2 eps][n_sig][T]
+    // the workspace's quad region holds the two energy rows and the four
+    // selections (2 x 8 + 4 x 4 = 32 bytes per (signal, frame))
+    double* en = w.Q;                         // [2 eps][n_sig][T]
     int* sel = (int*)(en + 2 * n_sig * T);    // [2 pct][2 eps][n_sig][T]
     const int64_t ST = n_sig * (int64_t)T;
     hipLaunchKernelGGL(frame_energy2_kernel, dim3((T + 3) / 4, (unsigned)n_sig), dim3(256), 0, s, P,

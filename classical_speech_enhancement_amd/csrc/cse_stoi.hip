@@ -61,7 +61,7 @@ constexpr int FB = 16;                   // most STFT frames per phase-A block
 constexpr int MAXD = 18;
 // block table (ints): D, j0, nf, p[MAXD], sa[FB + 1], sb[FB + 1].  A block takes
 // frames while nf <= FB and its OLA rows need <= MAXD distinct half-blocks
-// (a row needs at most 2, so every block but the last has >= 13 frames)
+// (a row needs at most 2, so every block but the last holds >= MINF = 8 frames)
 constexpr int T_D = 0, T_J0 = 1, T_NF = 2, T_P = 3, T_SA = T_P + MAXD, T_SB = T_SA + FB + 1;
 constexpr int BT = 72;
 static_assert(T_SB + FB + 1 <= BT, "block table size");
@@ -69,22 +69,16 @@ constexpr int MINF = MAXD / 2 - 1;       // frames every block but the last hold
 constexpr int META = 8;                  // ints per signal: K, M, J, ok, nblk
 constexpr int SLOTS = 9;                 // half-blocks resampled per pass (9 x 27 tasks <= 256)
 constexpr int GRP = 27;                  // phase groups (5 outputs) covering one half-block
-constexpr int SROW = 43;                 // staging: 8 rows (sample mod 8) x 43 columns
-// floats per staged slot (>= 8 SROW = 344); 347 = 27 (mod 64): the resampling
-// reads of lane tid = 27 s + g fall on bank tid + const (mod 64), so the
-// slots sharing a wave do not collide (344 collided on 3 banks per slot
-// boundary; 4,096 cells 4.30 / 4.35 -> 4.29 / 4.28 ms)
-#ifndef CSE_STOI_LIN
-#define CSE_STOI_LIN 1
-#endif
-// CSE_STOI_LIN (r05): the slot's samples in order, st[uu], so a phase group's 8
+// staging (r05): the slot's samples in order, st[uu], so a phase group's 8
 // samples of one tap block are 32 contiguous, aligned bytes: two ds_read_b128
 // instead of eight ds_read_b32 per block (the slot stride a multiple of 16 B).
-// 4,096 10-s cells, two alternating rounds: 4.55 / 4.50 -> 4.24 / 4.30 ms.
-// (CSE_STOI_LIN=0: 8 rows by sample mod 8, the stride below)
-constexpr int SSTR = CSE_STOI_LIN ? 344 : 347;
-static_assert(CSE_STOI_LIN ? (SSTR >= 8 * (GRP + 15) + 8 && SSTR % 4 == 0)
-                           : (SSTR >= 8 * SROW && SSTR % 64 == GRP), "staging slot stride");
+// 4,096 10-s cells, two alternating rounds: 4.55 / 4.50 -> 4.24 / 4.30 ms
+// against r04's 8 rows by sample mod 8 (43 columns, slot stride 347 = 27 mod 64
+// so that the slots sharing a wave did not collide; r06 removed that layout).
+// Slot strides 348 / 352 / 360 and blocks padded to 12 floats measured no
+// faster.
+constexpr int SSTR = 344;  // floats per staged slot
+static_assert(SSTR >= 8 * (GRP + 15) + 8 && SSTR % 4 == 0, "staging slot stride");
 // (r03's opt-in i8-sliced resampler on the matrix pipe, level with this fp64 FIR
 // at best, left the product in r04: tools/stoi_mf.md says how to rebuild it)
 constexpr int STAGE_F = SLOTS * SSTR;
@@ -540,7 +534,7 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                         const int uu = fr + FW * u;
                         float v = (unsigned)(fbase + FW * u) < (unsigned)cnt ? pre[u] : 0.0f;
                         if (clip) v = fminf(fmaxf(v, -1.0f), 1.0f);
-                        if (u < PF - 1 || uu < NU) st[CSE_STOI_LIN ? uu : (uu & 7) * SROW + (uu >> 3)] = v;
+                        if (u < PF - 1 || uu < NU) st[uu] = v;
                     }
                 }
                 __syncthreads();  // stage (and the next block's table) visible
@@ -554,9 +548,9 @@ __device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t le
                     const int64_t p = tb[T_P + c0 + s];
                     const int64_t q0 = (HOP * p) / UP;
                     const int64_t q = q0 + g;
-                    const float* st = L.u.a.stage + s * SSTR + (CSE_STOI_LIN ? 8 * g : g);
-                    // sample j of tap block kb (j < 8): st[8 kb + j] (LIN) or st[j SROW + kb]
-                    auto sidx = [](int kb, int j) { return CSE_STOI_LIN ? 8 * kb + j : j * SROW + kb; };
+                    const float* st = L.u.a.stage + s * SSTR + 8 * g;
+                    // sample j of tap block kb (j < 8): st[8 kb + j]
+                    auto sidx = [](int kb, int j) { return 8 * kb + j; };
                     double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
                     // taps kk = 8 kb + j of phase r; c_r[kk] = 0 outside
                     // 8r <= 5kk <= 8r + 580 (and kk >= 123): the edge blocks

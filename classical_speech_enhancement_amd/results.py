@@ -6,7 +6,7 @@ The reference's batch driver writes (speech_enhancement_comparison.py):
   - per algorithm means in summary/summary_means.json (_compute_and_save_summary
     :341-373);
   - summary/all_results.csv with a fixed header and "NA" for missing values
-    (:462-471, _fmt :267-270);
+    (:462-471, _fmt :273-276);
   - the three optimised waveforms per (pair, algorithm) as
     {stem}_{alg}_optimized_{stoi,pesq,balanced}.wav (:302-312; soundfile's
     default WAV subtype, PCM_16).

@@ -2,7 +2,7 @@
 
 The reference walks pairs -> algorithms -> parameter combinations one cell at
 a time (speech_enhancement_comparison.py:149-226 inside optimize_parameters,
-called per algorithm from run_algorithm_on_pair :275-292 and main :395-430).
+called per algorithm from run_algorithm_on_pair :278-294 and main :440-455).
 Here the whole (pair x algorithm x grid cell) set is one job:
 
   job_specs      the reference's enumeration order; a cell's index in this
@@ -28,7 +28,7 @@ Scores: the reference scores cells by STOI, PESQ and their balance
 (evaluation_metrics.py:39-58).  PESQ's C extension is not in this image, so
 the PESQ and balance objectives are not scored; STOI and SNR each get the
 reference's sequential selection (the reference itself skips a cell whose
-PESQ is None, :182-183 — that rule is dropped, or nothing would be selected).
+PESQ is None, speech_enhancement_comparison.py:180-181 — that rule is dropped, or nothing would be selected).
 Each cell is scored like finalize_enhanced (:92-106): its output is aligned
 to the clean reference by the cross-correlation lag (on the device,
 cse_xcorr_lag), length-matched, checked for finiteness and clipped, then

@@ -205,8 +205,9 @@ int cse_noise_percentile_med2(const double* P, const double* med, int64_t n_sig,
  * eps from one read of P, one sort of each eps's energies for both
  * percentiles, one order-statistic launch per percentile covering both eps.
  * N_pe (p: percentile a/b, e: eps a/b) equal cse_noise_percentile_med bit for
- * bit; a NULL output is skipped.  Uses the workspace's min-tracking IIR region
- * (run it after any min-tracking call on the same stream, as the engine does). */
+ * bit; a NULL output is skipped.  Its scratch is a region of the workspace of
+ * its own (r06: r05 borrowed the min-tracking IIR region); as for every
+ * cse_noise_* call, one workspace serves one stream at a time. */
 int cse_noise_percentile_quad(const double* P, const double* med, int64_t n_sig, int T, int B,
                               double percentile_a, double percentile_b, double eps_a,
                               double eps_b, float* N_aa, float* N_ab, float* N_ba, float* N_bb,

@@ -118,14 +118,15 @@ def test_job_units_match_shards():
 @pytest.mark.parametrize("n_fft", [512, 1024])
 def test_roofline_block_prices_the_committed_pmc(n_fft):
     """The line's VALU roofline from the committed PMC of this build
-    (profiles/pmc_enhance{n_fft}_r05.json, digest-matched), on the product
-    binary's own counts: frac = (2 x (VALU - TRANS) + 4 x TRANS) / (1024 SIMDs
-    x 2.4 GHz x kernel time) (a packed instruction counted once, at the scalar
-    rate); dense_at_occupancy = the same counts at the rates
-    tools/micro/valu_peak.hip measures at the kernel's waves per SIMD;
-    fp32_flops = SQ_INSTS_VALU_FLOPS_FP32 x 64 / time against 157.3 TF.  No
-    scalar-build pricing (r04's frac_vs_dense_stream) and no bandwidth derived
-    from SURVEY 8(d)'s nominal bytes."""
+    (profiles/pmc_enhance{n_fft}_<round>.json, digest-matched), every
+    instruction kind priced at the SIMD cycles it takes on a SIMD-32: f32 VALU
+    2, packed v_pk_*_f32 4 (two f32 operations per lane at the same 64
+    FLOP/clk/SIMD peak), transcendental 4, fp64 4 (r06; r05 priced a packed
+    instruction at 2).  frac = cycles / (1024 SIMDs x 2.4 GHz x kernel time);
+    the packed count is the measured one (scalar-build class counts minus the
+    product's), and it must agree with the FP32 FLOP counter; no
+    dense_at_occupancy block and no bandwidth derived from SURVEY 8(d)'s
+    nominal bytes."""
     import json
     units = 457237200
     pmc = bench.load_pmc(units, n_fft)
@@ -133,21 +134,24 @@ def test_roofline_block_prices_the_committed_pmc(n_fft):
         pytest.skip("no committed PMC profile of these kernel sources")
     ks_ms = pmc["kernel_ms"]
     r = bench.roofline_block(n_fft, units, ks_ms)
-    assert r["bound"].startswith("valu") and r["pmc_matches_build"]
-    assert "frac_vs_dense_stream" not in r
+    assert r["bound"] == "valu" and r["pmc_matches_build"]
+    assert "frac_vs_dense_stream" not in r and "dense_at_occupancy" not in r
     ks = ks_ms / 1e3
     v, t = pmc["sq_insts_valu"], pmc["sq_insts_valu_trans"]
-    need = 2 * (v - t) + 4 * t
+    pk, f64 = pmc["packed_insts"], pmc.get("sq_insts_valu_f64") or 0.0
+    need = 2 * (v - t - pk - f64) + 4 * (pk + t + f64)
     assert abs(r["frac"] - need / (bench.SIMDS * bench.CLOCK * ks)) < 1e-12
-    d = r.get("dense_at_occupancy")
-    if d:
-        fma, _, exp = bench.DENSE_CYC[pmc["waves_per_simd"]]
-        dense = fma * (v - t) + exp * t
-        assert abs(d["frac"] - dense / (bench.SIMDS * pmc["clock_ghz_profiled"] * 1e9 * ks)) < 1e-12
+    assert r["packed_insts"] == pk
+    if n_fft == 1024:
+        assert pk == 0  # the 1024 kernel is scalar f32
+    else:
+        assert pk > 0.5 * (v - t - f64)  # most of the 512 kernel's f32 work is packed
+        chk = pmc["packed"]["flop_check"]["ratio"]
+        assert abs(chk - 1) < 0.02, chk
     if pmc.get("sq_insts_valu_flops_fp32"):
         f = r["fp32_flops"]
         assert abs(f["frac"] - pmc["sq_insts_valu_flops_fp32"] * 64 / ks / 157.3e12) < 1e-12
         assert 0 < f["frac"] < 1
-    assert 0.2 < r["frac"] < 1.0
+    assert 0.3 < r["frac"] < 1.0
     assert all("GBps" not in k or (r[k] or 0) < 8000 for k in r)
     json.dumps(r)  # the line must serialise

@@ -5,10 +5,18 @@ and calls, and the PMC counters of the separate --pmc passes, per launch
 (counter sum over the profiled launches / launches).  HBM traffic per launch =
 (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 (gfx950 correction, MI355X_MICROARCH.md
 HBM/rocprofv3 section: FETCH_SIZE counts half the bytes of wide streaming reads).
-VALU issue fraction = (2 x (VALU - TRANS) + 4 x TRANS) SIMD cycles (fp64 FMA/MUL/ADD
-at 4) over 1024 SIMDs x SQ_BUSY_CYCLES / 32 (per-shader-engine cycles with
-waves resident, summed over the 32 SEs).  GRBM_GUI_ACTIVE / 8 read twice the
-shader clock on the r02 boxes, so it is only recorded.
+VALU lane-op cycles (r06 pricing, MI355X_MICROARCH.md / cdna_hip_programming.md:
+a wave64 f32 VALU instruction 2 SIMD cycles on a SIMD-32, a packed v_pk_*_f32
+4 (two f32 operations per lane: the FP32 peak is 64 FLOP/clk/SIMD for both
+forms), a transcendental 4, an fp64 FMA/MUL/ADD 4; calibrated chip-wide by
+tools/micro/valu_cal.hip) over 1024 SIMDs x SQ_BUSY_CYCLES / 32 (per-shader-
+engine cycles with waves resident, summed over the 32 SEs).  The packed
+instructions are counted, not assumed: the F32 class counters
+(SQ_INSTS_VALU_ADD/MUL/FMA_F32) count a v_pk_* once, so the scalar build of the
+same sources (CSE_PK=0, every f32 operation its own instruction) minus the
+product build gives the packed count per class; the FP32 FLOP counter (which
+counts a packed instruction's two operations) checks it.  GRBM_GUI_ACTIVE / 8
+read twice the shader clock on the r02 boxes, so it is only recorded.
 
     python tools/pmc_summary.py TAG ROUND [UNITS_512 UNITS_1024]
 
@@ -25,7 +33,42 @@ import sys
 REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 KERNELS = {"enhance512": "enhance_kernel<512, false>", "enhance1024": "enhance_kernel<1024, false>",
            "stoi": "stoi_cells_kernel", "xcorr_lag": "xcorr_lag_kernel"}
-SIMDS, VALU_CYC, TRANS_CYC = 1024, 2, 4  # transcendental = 2x v_fma_f32 (tools/micro/valu_rate.hip)
+SIMDS = 1024
+VALU_CYC, PK_CYC, TRANS_CYC, F64_CYC = 2, 4, 4, 4  # SIMD cycles per wave64 instruction (see above)
+F64_COUNTERS = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")
+
+
+def valu_cycles(vi, tr, pk, f64):
+    """SIMD cycles of a launch's VALU instructions: vi all VALU, of which tr
+    transcendental, pk packed f32, f64 fp64 FMA/MUL/ADD."""
+    return VALU_CYC * (vi - tr - pk - f64) + PK_CYC * pk + TRANS_CYC * tr + F64_CYC * f64
+
+
+def packed_counts(prod, scalar):
+    """Packed f32 instructions per class from the F32 class counters of the
+    product build (a v_pk_* counted once) and the scalar build (CSE_PK=0: two
+    instructions): {add, mul, fma, total, flop_check}.  flop_check compares the
+    product's FLOP counter with what its class counters and these packed counts
+    imply (FLOPS = ADD + MUL + 2 FMA + TRANS + pk_add + pk_mul + 2 pk_fma)."""
+    if not prod or not scalar:
+        return None
+    out = {}
+    for c, k in (("add", "SQ_INSTS_VALU_ADD_F32"), ("mul", "SQ_INSTS_VALU_MUL_F32"),
+                 ("fma", "SQ_INSTS_VALU_FMA_F32")):
+        if k not in prod or k not in scalar:
+            return None
+        out[c] = scalar[k] - prod[k]
+    out["total"] = out["add"] + out["mul"] + out["fma"]
+    fl = prod.get("SQ_INSTS_VALU_FLOPS_FP32")
+    if fl:
+        implied = (prod["SQ_INSTS_VALU_ADD_F32"] + prod["SQ_INSTS_VALU_MUL_F32"]
+                   + 2 * prod["SQ_INSTS_VALU_FMA_F32"] + prod.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
+                   + out["add"] + out["mul"] + 2 * out["fma"])
+        out["flop_check"] = {"flops_counter": fl, "implied_by_class_counts": implied,
+                             "ratio": implied / fl}
+    if "SQ_INSTS_VALU" in prod and "SQ_INSTS_VALU" in scalar:
+        out["valu_difference"] = scalar["SQ_INSTS_VALU"] - prod["SQ_INSTS_VALU"]
+    return out
 
 
 # WG<NFFT, false>::BYTES (dynamic LDS: the trace's LDS_Block_Size reads 0)
@@ -80,16 +123,15 @@ def counters(pattern, kname):
     return {c: sum(v) / len(v) for c, v in per.items()}, disp
 
 
-def derive(pmc, kernel_ms):
+def derive(pmc, kernel_ms, packed=None):
     d = {}
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         d["hbm_bytes_per_launch"] = (2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024
     vi, tr = pmc.get("SQ_INSTS_VALU"), pmc.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
-    f64 = sum(pmc.get(k, 0.0) for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
-                                         "SQ_INSTS_VALU_ADD_F64"))
+    f64 = sum(pmc.get(k, 0.0) for k in F64_COUNTERS)
     busy = pmc.get("SQ_BUSY_CYCLES")
     if vi and busy:
-        need = VALU_CYC * (vi - tr - f64) + TRANS_CYC * tr + 2 * VALU_CYC * f64
+        need = valu_cycles(vi, tr, packed or 0.0, f64)
         cyc = busy / 32
         d["valu_issue_cycles"] = need
         d["busy_cycles_per_se"] = cyc
@@ -138,12 +180,11 @@ def main(tag, rnd, units512=None, units1024=None):
                 ms = v["avg_ms"]
         pmc, nd = counters(os.path.join(base, f"pmc_{pmcname}_*", "run_counter_collection.csv"), kname)
         summary["kernels"][key] = {"kernel": kname, "kernel_ms_rocprof": ms, "pmc_per_launch": pmc,
-                                   "pmc_launches": nd, **derive(pmc, ms)}
-    # r05: the product binary's own counts are the basis (a packed v_pk_*
-    # instruction counted once: it issues at the scalar rate); the SQPK pass
-    # adds its FP32 FLOPs.  r04 priced the scalar build (CSE_PK=0) instead,
-    # which counts instructions the product does not issue; that build's passes
-    # are still summarised when present, as a record only.
+                                   "pmc_launches": nd}
+    # r06: the product build's counts priced per instruction kind, the packed
+    # count from the F32 class counters of the product and of the scalar build
+    # (CSE_PK=0; the n_fft 1024 kernel issues no packed instruction: its ISA
+    # has no v_pk_*, `python tools/isa_sections.py enhance_kernelILi1024ELb0E`)
     for key, name, pk in (("enhance512", "512", "pk512"), ("enhance1024", "1024", "pk1024")):
         k = summary["kernels"][key]
         occ = occupancy(os.path.join(base, f"kt_{name}", "run_kernel_trace.csv"), KERNELS[key])
@@ -153,13 +194,13 @@ def main(tag, rnd, units512=None, units1024=None):
         if ppk:
             k["pmc_packed_counters_per_launch"] = ppk
             k["flops_fp32"] = ppk.get("SQ_INSTS_VALU_FLOPS_FP32")
-    k512 = summary["kernels"]["enhance512"]
-    spmc, _ = counters(os.path.join(base, "pmc_s512_sq1", "run_counter_collection.csv"), KERNELS["enhance512"])
-    spk, _ = counters(os.path.join(base, "pmc_s512_pk", "run_counter_collection.csv"), KERNELS["enhance512"])
-    ppk, _ = counters(os.path.join(base, "pmc_pk512", "run_counter_collection.csv"), KERNELS["enhance512"])
-    if spmc:  # record only (see above)
-        k512["pmc_scalar_build_per_launch"] = spmc
-        k512["pmc_scalar_build_pk_pass_per_launch"] = spk
+        spk, _ = counters(os.path.join(base, f"pmc_s{name}_pk", "run_counter_collection.csv"), KERNELS[key])
+        if spk:
+            k["pmc_scalar_build_pk_pass_per_launch"] = spk
+        k["packed"] = packed_counts(ppk, spk) if name == "512" else {"total": 0.0, "source": "ISA"}
+    for key, k in summary["kernels"].items():
+        pk = (k.get("packed") or {}).get("total") if key.startswith("enhance") else 0.0
+        k.update(derive(k["pmc_per_launch"], k["kernel_ms_rocprof"], pk))
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
     json.dump(summary, open(os.path.join(REPO, "profiles", f"{rnd}_kernels.json"), "w"), indent=1)
     for key, units in (("enhance512", units512), ("enhance1024", units1024)):
@@ -176,7 +217,12 @@ def main(tag, rnd, units512=None, units1024=None):
                "sq_insts_valu_flops_fp32": k.get("flops_fp32"),
                "valu_frac": k.get("valu_frac"), "clock_ghz_profiled": k.get("clock_ghz_profiled"),
                "valu_issue_cycles": k.get("valu_issue_cycles"),
-               "valu_issue_cycles_source": "this build's own SQ_INSTS_VALU / _TRANS_F32 (packed counted once)",
+               "valu_issue_cycles_source": ("this build's SQ_INSTS_VALU priced per kind: f32 VALU 2, "
+                                            "packed v_pk_* 4, transcendental 4, f64 FMA/MUL/ADD 4 cycles"),
+               "packed_insts": (k.get("packed") or {}).get("total"),
+               "packed": k.get("packed"),
+               "sq_insts_valu_f64": sum(pmc.get(c, 0.0) for c in F64_COUNTERS) if any(
+                   c in pmc for c in F64_COUNTERS) else None,
                "vgprs": k.get("vgprs"), "lds_bytes": k.get("lds_bytes"),
                "waves_per_simd": k.get("waves_per_simd"),
                "share_wait_inst_any": k.get("share_wait_inst_any"),

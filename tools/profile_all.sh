@@ -5,6 +5,8 @@
 #   enhance_kernel<1024> : bench.py --nfft 1024
 #   stoi_cells_kernel, xcorr_*: tools/bench_sweep.py (full grid, 4 pairs)
 #     bash tools/profile_all.sh TAG [what...]     what in {kt512, kt1024, ktsweep, pmc512, pmc1024, pmcstoi, pmcpk, pmcpk1024, pmclds, pmclds1024, pmc512s}
+# (pmc512s needs the scalar build: python -c "import __graft_entry__ as g;
+#  g.build(out='classical_speech_enhancement_amd/libcse_scalar.so', defines=['CSE_PK=0'])")
 # Output under gpurun_out/prof_TAG/; tools/pmc_summary.py turns it into profiles/*.json.
 set -o pipefail
 TAG=${1:-dev}
@@ -27,8 +29,9 @@ SQLDS="SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_W
 SQF64="SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
 # r04: how the counters see packed f32 (v_pk_*) instructions
 SQPK="SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_FLOPS_FP32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
-# the scalar build of the same sources (CSE_PK=0): the VALU issue cycles of
-# the arithmetic with every f32 operation its own instruction
+# the scalar build of the same sources (CSE_PK=0, every f32 operation its own
+# instruction): its F32 class counts minus the product's are the product's
+# packed instructions per class (tools/pmc_summary.py packed_counts)
 SCALAR_LIB=${SCALAR_LIB:-classical_speech_enhancement_amd/libcse_scalar.so}
 
 kt() {  # name, command...
@@ -48,15 +51,15 @@ for w in $WHAT; do
     kt1024) kt 1024 $B1024 ;;
     ktsweep) kt sweep $SWEEP ;;
     pmc512) pmc 512_fetch FETCH_SIZE $P512 && pmc 512_write WRITE_SIZE $P512 &&
-            pmc 512_sq1 "$SQ1" $P512 && pmc 512_sq2 "$SQ2" $P512 ;;
+            pmc 512_sq1 "$SQ1" $P512 && pmc 512_sq2 "$SQ2" $P512 && pmc 512_f64 "$SQF64" $P512 ;;
     pmc1024) pmc 1024_fetch FETCH_SIZE $P1024 && pmc 1024_write WRITE_SIZE $P1024 &&
-             pmc 1024_sq1 "$SQ1" $P1024 && pmc 1024_sq2 "$SQ2" $P1024 ;;
+             pmc 1024_sq1 "$SQ1" $P1024 && pmc 1024_sq2 "$SQ2" $P1024 && pmc 1024_f64 "$SQF64" $P1024 ;;
     pmcstoi) pmc stoi_f64 "$SQF64" $SWEEP && pmc stoi_sq2 "$SQ2" $SWEEP ;;
     pmcpk) pmc pk512 "$SQPK" $P512 ;;
     pmclds) pmc 512_lds "$SQLDS" $P512 ;;
     pmclds1024) pmc 1024_lds "$SQLDS" $P1024 ;;
     pmcpk1024) pmc pk1024 "$SQPK" $P1024 ;;
-    pmc512s) CSE_LIB=$SCALAR_LIB pmc s512_sq1 "$SQ1" $P512 && CSE_LIB=$SCALAR_LIB pmc s512_pk "$SQPK" $P512 ;;
+    pmc512s) CSE_LIB=$SCALAR_LIB pmc s512_pk "$SQPK" $P512 ;;
     *) echo "unknown $w"; exit 1 ;;
   esac
 done
