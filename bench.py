@@ -56,11 +56,19 @@ METRIC = ("STFT frame-gain evals/sec/node, 16kHz 512-pt FFT full grid; 1/2/4/8-G
 HBM_PEAK = 8.0e12              # MI355X_MICROARCH.md: 8.0 TB/s spec
 SIMDS = 1024                   # 256 CUs x 4 SIMD-32
 FP32_PEAK = 157.3e12           # MI355X_MICROARCH.md: FP32 vector, spec (64 FLOP/clk/SIMD)
-# SIMD cycles per wave64 VALU instruction (MI355X_MICROARCH.md, cdna_hip_programming.md:
-# v_fma_f32 2 on a SIMD-32; v_pk_*_f32 4, two f32 operations per lane at the same
-# 64 FLOP/clk/SIMD; transcendental 4; fp64 FMA/MUL/ADD 4 at 78.6 TF), checked
-# chip-wide by tools/micro/valu_cal.hip (profiles/r06_micro_valu_cal.json)
-VALU_CYC, PK_CYC, TRANS_CYC, F64_CYC = 2, 4, 4, 4
+# SIMD cycles per wave64 VALU instruction, measured chip-wide at 8 waves/SIMD
+# (tools/micro/valu_cal.hip, tools/micro/valu_mix.hip, HIP-event timed;
+# profiles/r06_micro_valu_cal.json, r06_micro_valu_mix.txt): a packed v_pk_*_f32
+# 4.0-4.2 and never overlapped by another VALU instruction (v_pk_fma_f32 153 TF =
+# the 157.3 TF FP32 peak); a transcendental 8.1, also exclusive (v_fma_f32 and
+# v_exp_f32 interleaved cost 4 + 8); an fp64 FMA 4.1-4.5; scalar f32 instructions
+# of the SIMD's two halves issue in parallel (v_add/v_mul/v_mov/v_add_u32 streams
+# 2.3-2.5, v_fma_f32 interleaved with v_add/v_mul/v_max 2.3-2.5 per instruction,
+# a pure v_fma_f32 or v_max_f32 stream 4).  Scalar f32 is priced at the parallel
+# rate, 2 (the guide's SIMD-32 figure, a lower bound on what the kernel's scalar
+# instructions take).  The guide's transcendental price (4) is reported beside it.
+VALU_CYC, PK_CYC, TRANS_CYC, F64_CYC = 2, 4, 8, 4
+GUIDE_TRANS_CYC = 4
 CLOCK = 2.4e9                  # max shader clock
 TOL = 1e-5                     # north-star relative waveform tolerance
 SNR_TOL_DB = 2e-4              # per-cell SNR tolerance of the parity tests
@@ -667,6 +675,11 @@ def valu_calibration():
         if r["waves_per_simd"] in (3, 8):
             out[f'{r["op"]}@{r["waves_per_simd"]}w'] = {"TFLOPs": round(r["tflops"], 2),
                                                           "cycles_per_wave_inst": round(r["cycles_per_wave_inst"], 3)}
+    mix = json.load(open(path)).get("mix") or {}
+    keep = ("v_fma_f32(vvv) + v_fma_f32(vvv)", "v_add_f32 + v_add_f32", "v_fma_f32(vvv) + v_add_f32",
+            "v_fma_f32(vvv) + v_max_f32", "v_fma_f32(vvv) + v_pk_fma_f32", "v_fma_f32(vvv) + v_exp_f32",
+            "v_pk_fma_f32 + v_exp_f32", "v_fma_f32(vvv) + v_fma_f64")
+    out["mix_cycles_per_wave_inst_8w"] = {k: mix[k].get("8") for k in keep if k in mix}
     return out
 
 
@@ -675,10 +688,10 @@ def roofline_block(n_fft, units, kern_ms):
 
     The product binary's own instruction counts (PMC of this launch size and
     n_fft, committed under profiles/ and matched to this build by a digest of
-    the kernel sources and flags), each priced at what it holds a SIMD-32
-    (VALU_CYC, PK_CYC, TRANS_CYC, F64_CYC: f32 VALU 2 cycles, packed v_pk_*_f32
-    4 since it carries two f32 operations per lane at the same 64 FLOP/clk/SIMD
-    peak, transcendental 4, fp64 4), over the live HIP-event kernel time:
+    the kernel sources and flags), each priced at the SIMD cycles the
+    chip-wide micro-benchmarks measure for its kind (VALU_CYC, PK_CYC,
+    TRANS_CYC, F64_CYC: f32 VALU 2, packed v_pk_*_f32 4, transcendental 8,
+    fp64 4), over the live HIP-event kernel time:
     `achieved` = those SIMD cycles per second, `peak` = 1024 SIMDs x 2.4 GHz.
     The packed count is measured (tools/pmc_summary.py: the F32 class counters
     of the scalar build CSE_PK=0 minus the product's, checked by the FLOP
@@ -695,9 +708,10 @@ def roofline_block(n_fft, units, kern_ms):
     ks = kern_ms / 1e3
     nominal = units * bytes_per_unit
     roof = {"bound": "valu",
-            "bound_note": ("VALU lane-op throughput: every VALU instruction of the launch priced at the "
-                           "SIMD cycles it takes (f32 2, packed f32 4, transcendental 4, f64 4 per wave64 "
-                           "instruction on a SIMD-32); HBM traffic is 2 % of peak"),
+            "bound_note": ("VALU throughput: every VALU instruction of the launch priced at the SIMD "
+                           "cycles a dense stream of its kind takes on this part (f32 2, packed f32 4, "
+                           "transcendental 8, f64 4 per wave64 instruction; tools/micro/valu_cal.hip, "
+                           "valu_mix.hip); HBM traffic is 2 % of peak"),
             "achieved": None,
             "peak": SIMDS * CLOCK / 1e9,
             "unit": "G SIMD VALU cycles/s (1024 SIMDs x 2.4 GHz)", "frac": None, "traffic": None,
@@ -741,6 +755,8 @@ def roofline_block(n_fft, units, kern_ms):
         roof["f64_insts"] = f64
         roof["cycles_per"] = {"f32_valu": VALU_CYC, "packed_f32": PK_CYC, "transcendental": TRANS_CYC,
                               "f64": F64_CYC}
+        guide = need - (TRANS_CYC - GUIDE_TRANS_CYC) * tr
+        roof["frac_transcendental_at_4"] = guide / ks / (SIMDS * CLOCK)
         if pmc.get("packed"):
             roof["packed_source"] = {k: pmc["packed"].get(k) for k in ("add", "mul", "fma", "flop_check",
                                                                         "valu_difference")}

@@ -303,6 +303,15 @@ struct WG {
     static constexpr bool ROT_TABLE = R2;
     static constexpr int ROTSTR = 80;
     static constexpr int OFF_LC = OFF_TW + (ROTOR_TW ? G::L * 48 : TWL * 144);
+    // sweep kernels (M2C, r06): bin M/2 of the slot group's cells is evaluated
+    // by one wave per frame (wave t mod 4 evaluates frame t + 1 for all the
+    // group's cells, one lane each) instead of by every lane of every cell.
+    // Its decision-directed state and Z'[M/2] live, at 512, in the unused tail
+    // of the twiddle table row of the cell's index (entries 15 and 16 / 17;
+    // pass 1 reads entries 0..15 and uses 0..14), at 1024 in a region of its
+    // own after the window table (160 B)
+    static constexpr bool M2C = !OUT;
+
     static constexpr int OFF_CP = OFF_LC + G::L * (ROT_TABLE ? ROTSTR : 8);  // CellParam[CPWG]
     // synthesis window w(n)/(NFFT wss(n)) at the lane's 32 (16) sample slots,
     // wss the steady-state window-square sum of this workgroup's hop (librosa's
@@ -311,7 +320,15 @@ struct WG {
     static constexpr int WSLOTS = HALF_TABLES ? 16 : 32;
     static constexpr int WSTR = HALF_TABLES ? 20 : 36;
     static constexpr int OFF_WIN = OFF_CP + CPWG * 32;
-    static constexpr int BYTES = OFF_WIN + G::L * WSTR * 4;
+    static constexpr int OFF_M2 = OFF_WIN + G::L * WSTR * 4;
+    static constexpr int BYTES = OFF_M2 + ((M2C && !R2) ? ((CPWG * 20 + 15) / 16) * 16 : 0);
+    static constexpr int m2r(int c) {  // float rr of cell c
+        return R2 ? OFF_TW + 144 * c + 120 : OFF_M2 + 16 * CPWG + 4 * c;
+    }
+    static constexpr int m2z(int c, int par) {  // f2 Z'[M/2] of cell c, frame parity par
+        return R2 ? OFF_TW + 144 * c + 128 + 8 * par : OFF_M2 + 16 * c + 8 * par;
+    }
+    static_assert(!M2C || (WAVES == 4 && (!R2 || (CPWG <= TWL && !ROTOR_TW))), "M2C layout");
     static constexpr int YPT = (G::B + THREADS - 1) / THREADS;     // Y/N elements per thread
     static constexpr int CPT = (HMAX + THREADS - 1) / THREADS;     // clean samples per thread
 };
@@ -500,7 +517,7 @@ __device__ __forceinline__ f2 gain_pair(f2 gam, f2 d, f2 a, f2& rr, float alpha_
 // mirror lane.  Bin M/2 (the 17th item) stays scalar (gain_bin).  Rows: Y
 // records (Y_p, Y_{M-p}) (16 B), (g_p, g_{M-p}, d_p, d_{M-p}) (16 B) and
 // MMSE's / SS's a pairs (8 B).  Packing rotors: the lane's table row.
-template <int NFFT, int ALGO, bool OUT>
+template <int NFFT, int ALGO, bool OUT, bool M2C>
 __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
                                              const void* __restrict__ growv,
                                              const float2* __restrict__ a2row, f2 (&z)[16],
@@ -522,10 +539,12 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
     float2 ac = WANT_A ? a2[0] : make_float2(0.0f, 0.0f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        // next pair's rows (j = 7: bin M/2, the record of pair M/2)
+        // next pair's rows (j = 7: bin M/2, the record of pair M/2, unless
+        // another wave evaluates it, M2C)
         const int nx = (j < 7) ? L * (j + 1) : M / 2 - i;
-        const float4 yn = y4[nx], gn = ldg(nx);
-        const float2 an = WANT_A ? a2[nx] : make_float2(0.0f, 0.0f);
+        const bool nxt = j < 7 || !M2C;
+        const float4 yn = nxt ? y4[nx] : float4{}, gn = nxt ? ldg(nx) : float4{};
+        const float2 an = (WANT_A && nxt) ? a2[nx] : make_float2(0.0f, 0.0f);
         f2 ya = f2{yc.x, yc.y}, yb = f2{yc.z, yc.w};
         f2 g;  // the pair's gains
         f2 s;  // the real factors of S = Y s (SS: sqrt(Ps) on the unit phasor)
@@ -560,12 +579,14 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
         gc = gn;
         ac = an;
     }
-    // bin M/2: scalar, Z'[M/2] = 2 conj(X_{M/2})
-    float2 ym = make_float2(yc.x, yc.y);
-    float gm;
-    const float sm = 2.0f * gain_bin<NFFT, ALGO>(ym, RowV{gc.x, gc.z, ac.x}, rrm, alpha_t, cpar, gm);
-    if (OUT && gout_row && i == 0) gout_row[M / 2] = gm;
-    xw[8] = f2{ym.x * sm, -ym.y * sm};
+    // bin M/2: scalar, Z'[M/2] = 2 conj(X_{M/2}) (M2C: run_wg's m2_eval)
+    if constexpr (!M2C) {
+        float2 ym = make_float2(yc.x, yc.y);
+        float gm;
+        const float sm = 2.0f * gain_bin<NFFT, ALGO>(ym, RowV{gc.x, gc.z, ac.x}, rrm, alpha_t, cpar, gm);
+        if (OUT && gout_row && i == 0) gout_row[M / 2] = gm;
+        xw[8] = f2{ym.x * sm, -ym.y * sm};
+    }
 }
 
 // One frame's gain stage + real-IFFT packing for one lane.
@@ -587,7 +608,7 @@ __device__ __forceinline__ void gain_pack_pk(const float4* __restrict__ y4row,
 // are __restrict__, so the scheduler may issue the bins' reads up front and
 // interleave the independent gain chains.  The packing rotors e^{2πi (i + L j)/NFFT}
 // come from the lane's LDS row (8 complex).
-template <int NFFT, int ALGO, bool OUT>
+template <int NFFT, int ALGO, bool OUT, bool M2C>
 __device__ __forceinline__ void gain_pack(const float2* __restrict__ yrow,
                                           const void* __restrict__ growv,
                                           const float* __restrict__ arow, cf (&z)[16],
@@ -637,6 +658,9 @@ __device__ __forceinline__ void gain_pack(const float2* __restrict__ yrow,
         if (j < 7) {
             ld(false, L * (j + 1), yan, gan);
             ld(true, L * (6 - j), ybn, gbn);
+        } else if (M2C) {  // bin M/2: another wave evaluates it (run_wg's m2_eval)
+            yan = make_float2(0.0f, 0.0f);
+            gan = RowV{0.0f, 0.0f, 0.0f};
         } else {
             // bin M/2 (the same for every lane): base - i + M/2
             yan = yrow[M / 2];
@@ -685,10 +709,12 @@ __device__ __forceinline__ void gain_pack(const float2* __restrict__ yrow,
             gb = gbn;
         }
     }
-    float gm;
-    const float sm = 2.0f * gain_bin<NFFT, ALGO>(ya, ga, rr[16], alpha_t, cpar, gm);
-    if (OUT && gout_row && i == 0) gout_row[M / 2] = gm;
-    xw[8] = cmk(ya.x * sm, -ya.y * sm);
+    if constexpr (!M2C) {
+        float gm;
+        const float sm = 2.0f * gain_bin<NFFT, ALGO>(ya, ga, rr[16], alpha_t, cpar, gm);
+        if (OUT && gout_row && i == 0) gout_row[M / 2] = gm;
+        xw[8] = cmk(ya.x * sm, -ya.y * sm);
+    }
 }
 
 // Position inside a frame (relative to the lane's first sample) of the lane's
@@ -976,6 +1002,65 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
     store_rows(0);
     load_rows(1);
 
+    // M2C: bin M/2 of frame tt for the workgroup's cells (lane c < CPWG: cell
+    // c) from that bin's Y and noise-row value, with the stager's and
+    // gain_pack_pk's arithmetic; writes Z'[M/2] and the state to the cell's
+    // table-row tail (read by the cell's lane 0 / the next frame's wave)
+    float2 m2y = make_float2(0.0f, 0.0f);
+    float m2n = 0.0f;
+    // (the same ranges as the row loads' resources, which are empty at 1024)
+    const __amdgpu_buffer_rsrc_t m2yrc = ROWS_BUF ? yrc : __builtin_amdgcn_make_buffer_rsrc(
+        (void*)Ybase, (short)0, W::M2C ? nf * B * 8 : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t m2nrc = ROWS_BUF ? nrc : __builtin_amdgcn_make_buffer_rsrc(
+        (void*)Nbase, (short)0, W::M2C ? ((nstride ? (nf - 1) * nstride : 0) + B) * 4 : 0, 0x00020000);
+    auto m2_load = [&](int tt) {  // bin M/2 of frame tt (0 past the rows' end)
+        m2y = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(
+            m2yrc, opaque_off(8 * (tt * B + M / 2)), 0, 0));
+        m2n = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+            m2nrc, opaque_off(4 * (tt * nstride + M / 2)), 0, 0));
+    };
+    auto m2_eval = [&](int tt) {
+        const int c = lane < W::CPWG ? lane : 0;
+        const float2 y = m2y;
+        const float P = y.x * y.x + y.y * y.y;
+        float2 yv = y;
+        RowV rv{0.0f, 0.0f, 0.0f};
+        if (!W::R2) {  // store_rows at 1024: Y itself and gamma (N for SS)
+            const float gam = fmaxf(P * m2n, EPS);
+            rv.g = (ALGO == CSE_ALGO_SS) ? m2n : (ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam);
+        } else if (ALGO == CSE_ALGO_SS) {  // store_rows: the phasor, (N, P)
+            const float sc = fmaxf(fabsf(y.x), fabsf(y.y)) < 0x1p-50f ? 0x1p64f : 1.0f;
+            const float yx = y.x * sc, yy = y.y * sc;
+            const float pz = fmaf(yx, yx, yy * yy);
+            const float r = __builtin_amdgcn_rsqf(pz);
+            yv = pz > 0.0f ? make_float2(yx * r, yy * r)
+                           : (pz == 0.0f ? make_float2(1.0f, 0.0f) : make_float2(pz - pz, pz - pz));
+            rv.g = m2n;
+            rv.d = P;
+        } else {
+            const float gam = fmaxf(P * m2n, EPS);
+            rv.g = ALGO == CSE_ALGO_OMLSA ? gam * kLog2e : gam;
+            rv.d = fmaxf(gam - 1.0f, 0.0f);
+            if (ALGO == CSE_ALGO_MMSE) rv.a = 0.88622692545275801f * fast_rcp(gam + 1e-12f);
+        }
+        const CellParam cp = *(const CellParam*)(smem + W::OFF_CP + 32 * c);
+        float rr = tt == 0 ? 0.0f : *(const float*)(smem + W::m2r(c));
+        float gm;
+        const float sm = 2.0f * gain_bin<NFFT, ALGO>(yv, rv, rr, tt == 0 ? 0.0f : cp.p0, cp, gm);
+        if (lane < W::CPWG) {
+            *(f2*)(smem + W::m2z(c, tt & 1)) = f2{yv.x * sm, -yv.y * sm};
+            *(float*)(smem + W::m2r(c)) = rr;
+        }
+    };
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    if constexpr (W::M2C) {
+        if (wave_u == 0) {  // frame 0 (visible at the loop's first barrier)
+            m2_load(0);
+            m2_eval(0);
+        }
+        m2_load(wave_u + 1);  // wave w's first turn is frame w: it evaluates frame w + 1
+    }
+
     const int b2 = (L == 16) ? i : (i & 15);
     const int h2 = (L == 16) ? 0 : (i >> 4);
     // lane's first sample offset inside a frame
@@ -1031,7 +1116,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 const float alpha_t = (t == 0) ? 0.0f : cpar.p0;
                 const int yb = W::OFF_Y + (t & 1) * W::YROW, gb = W::OFF_G + (t & 1) * W::GROW;
                 const int ab = W::OFF_A + (t & 1) * W::AROW;
-                gain_pack_pk<NFFT, ALGO, OUT>((const float4*)(smem + yb), (const void*)(smem + gb),
+                gain_pack_pk<NFFT, ALGO, OUT, W::M2C>((const float4*)(smem + yb), (const void*)(smem + gb),
                                               (const float2*)(smem + ab), z, (f2*)(smem + creg + 72 * i),
                                               rr2, rrm, alpha_t, cpar,
                                               (const float4*)(smem + W::OFF_LC + W::ROTSTR * i),
@@ -1049,9 +1134,22 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 const f2* xd = (const f2*)(smem + opaque_off(xo + 8));
 #pragma unroll
                 for (int s = 8; s < 16; ++s) z[s] = ((15 - s) & 1) ? xd[14 - s] : xe[15 - s];
+                if constexpr (W::M2C) {  // lane 0: Z'[M/2] from the frame's evaluating wave
+                    const f2 zm = *(const f2*)(smem + W::m2z(cslot, t & 1));
+                    if (i == 0) z[8] = zm;
+                }
             }
             CSE_MARK("rows");
             store_rows(t + 1);
+            if constexpr (W::M2C) {
+                // this frame's wave evaluates bin M/2 of frame t + 1 for every
+                // cell (before load_rows: its operands' wait covers no new load)
+                // and fetches the operands of its next turn, frame t + 5
+                if (wave_u == (t & 3)) {
+                    if (t + 1 < nf) m2_eval(t + 1);
+                    m2_load(t + 5);
+                }
+            }
             load_rows(t + 2);
             CSE_MARK("pass1");
             {  // pass-1 twiddles from the lane's table row (8 ds_read_b128), issued ahead of the DFT
@@ -1110,7 +1208,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 // Z'[M - i - L e] (e < 8) and Z'[M/2] (e = 8); lane q takes
                 // z[s] (s >= 8) = Z'[q + L s] from lane (L - q) mod L, entry 15 - s
                 // (lane 0: its own entry 16 - s, entry 8 = Z'[M/2] for s = 8)
-                gain_pack<NFFT, ALGO, OUT>(
+                gain_pack<NFFT, ALGO, OUT, W::M2C>(
                     (const float2*)(smem + yb), (const void*)(smem + gb),
                     (const float*)(smem + ab), z, (cf*)(smem + creg + 72 * i), rr, alpha_t, cpar,
                     (const float4*)(smem + W::OFF_LC + W::ROTSTR * i),
@@ -1125,9 +1223,19 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
                 const cf* xr = (const cf*)(smem + creg + 72 * partner + (i == 0 ? 8 : 0));
 #pragma unroll
                 for (int s = 8; s < 16; ++s) z[s] = xr[15 - s];
+                if constexpr (W::M2C) {  // lane 0: Z'[M/2] from the frame's evaluating wave
+                    const f2 zm = *(const f2*)(smem + W::m2z(cslot, t & 1));
+                    if (i == 0) z[8] = cmk(zm.x, zm.y);
+                }
             }
             CSE_MARK("rows");
             store_rows(t + 1);  // other buffer: its last readers passed this frame's barrier
+            if constexpr (W::M2C) {  // see the packed branch
+                if (wave_u == (t & 3)) {
+                    if (t + 1 < nf) m2_eval(t + 1);
+                    m2_load(t + 5);
+                }
+            }
             load_rows(t + 2);
 
             CSE_MARK("pass1");

@@ -119,10 +119,10 @@ def test_job_units_match_shards():
 def test_roofline_block_prices_the_committed_pmc(n_fft):
     """The line's VALU roofline from the committed PMC of this build
     (profiles/pmc_enhance{n_fft}_<round>.json, digest-matched), every
-    instruction kind priced at the SIMD cycles it takes on a SIMD-32: f32 VALU
-    2, packed v_pk_*_f32 4 (two f32 operations per lane at the same 64
-    FLOP/clk/SIMD peak), transcendental 4, fp64 4 (r06; r05 priced a packed
-    instruction at 2).  frac = cycles / (1024 SIMDs x 2.4 GHz x kernel time);
+    instruction kind priced at the SIMD cycles the chip-wide micro-benchmarks
+    measure (tools/micro/valu_cal.hip, valu_mix.hip): f32 VALU 2, packed
+    v_pk_*_f32 4, transcendental 8, fp64 4 (r06; r05 priced a packed
+    instruction at 2 and a transcendental at 4).  frac = cycles / (1024 SIMDs x 2.4 GHz x kernel time);
     the packed count is the measured one (scalar-build class counts minus the
     product's), and it must agree with the FP32 FLOP counter; no
     dense_at_occupancy block and no bandwidth derived from SURVEY 8(d)'s
@@ -139,7 +139,7 @@ def test_roofline_block_prices_the_committed_pmc(n_fft):
     ks = ks_ms / 1e3
     v, t = pmc["sq_insts_valu"], pmc["sq_insts_valu_trans"]
     pk, f64 = pmc["packed_insts"], pmc.get("sq_insts_valu_f64") or 0.0
-    need = 2 * (v - t - pk - f64) + 4 * (pk + t + f64)
+    need = 2 * (v - t - pk - f64) + 4 * (pk + f64) + 8 * t
     assert abs(r["frac"] - need / (bench.SIMDS * bench.CLOCK * ks)) < 1e-12
     assert r["packed_insts"] == pk
     if n_fft == 1024:

@@ -12,6 +12,9 @@
 //   v_add_f32      1 FLOP per lane
 //   v_exp_f32      transcendental
 //   v_fma_f64      2 FLOP per lane
+// Every op takes the loop-invariant scalar s as an SGPR operand (tools/micro/
+// valu_mix.hip: VGPR-only v_add_f32 / v_mul_f32 streams issue at 2.3-2.5
+// cycles, the SGPR forms at 4).
 // The launch is timed by HIP events (the whole chip, 256 CUs x 4 SIMDs x W
 // waves); the clock the part held is s_memtime / s_memrealtime (100 MHz) of
 // each workgroup's loop.  Printed per (op, W): ms, TFLOP/s (lane-op rate for

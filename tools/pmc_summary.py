@@ -5,11 +5,10 @@ and calls, and the PMC counters of the separate --pmc passes, per launch
 (counter sum over the profiled launches / launches).  HBM traffic per launch =
 (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 (gfx950 correction, MI355X_MICROARCH.md
 HBM/rocprofv3 section: FETCH_SIZE counts half the bytes of wide streaming reads).
-VALU lane-op cycles (r06 pricing, MI355X_MICROARCH.md / cdna_hip_programming.md:
-a wave64 f32 VALU instruction 2 SIMD cycles on a SIMD-32, a packed v_pk_*_f32
-4 (two f32 operations per lane: the FP32 peak is 64 FLOP/clk/SIMD for both
-forms), a transcendental 4, an fp64 FMA/MUL/ADD 4; calibrated chip-wide by
-tools/micro/valu_cal.hip) over 1024 SIMDs x SQ_BUSY_CYCLES / 32 (per-shader-
+VALU cycles (r06 pricing, measured chip-wide by tools/micro/valu_cal.hip and
+valu_mix.hip, see bench.py: a wave64 f32 VALU instruction 2 SIMD cycles, a
+packed v_pk_*_f32 4, a transcendental 8, an fp64 FMA/MUL/ADD 4) over 1024
+SIMDs x SQ_BUSY_CYCLES / 32 (per-shader-
 engine cycles with waves resident, summed over the 32 SEs).  The packed
 instructions are counted, not assumed: the F32 class counters
 (SQ_INSTS_VALU_ADD/MUL/FMA_F32) count a v_pk_* once, so the scalar build of the
@@ -34,7 +33,7 @@ REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 KERNELS = {"enhance512": "enhance_kernel<512, false>", "enhance1024": "enhance_kernel<1024, false>",
            "stoi": "stoi_cells_kernel", "xcorr_lag": "xcorr_lag_kernel"}
 SIMDS = 1024
-VALU_CYC, PK_CYC, TRANS_CYC, F64_CYC = 2, 4, 4, 4  # SIMD cycles per wave64 instruction (see above)
+VALU_CYC, PK_CYC, TRANS_CYC, F64_CYC = 2, 4, 8, 4  # SIMD cycles per wave64 instruction (see above)
 F64_COUNTERS = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")
 
 
@@ -72,7 +71,7 @@ def packed_counts(prod, scalar):
 
 
 # WG<NFFT, false>::BYTES (dynamic LDS: the trace's LDS_Block_Size reads 0)
-LDS_BYTES = {"enhance_kernel<512, false>": 53600, "enhance_kernel<1024, false>": 52800}
+LDS_BYTES = {"enhance_kernel<512, false>": 53600, "enhance_kernel<1024, false>": 52960}
 
 
 def occupancy(trace, kname):
@@ -218,7 +217,7 @@ def main(tag, rnd, units512=None, units1024=None):
                "valu_frac": k.get("valu_frac"), "clock_ghz_profiled": k.get("clock_ghz_profiled"),
                "valu_issue_cycles": k.get("valu_issue_cycles"),
                "valu_issue_cycles_source": ("this build's SQ_INSTS_VALU priced per kind: f32 VALU 2, "
-                                            "packed v_pk_* 4, transcendental 4, f64 FMA/MUL/ADD 4 cycles"),
+                                            "packed v_pk_* 4, transcendental 8, f64 FMA/MUL/ADD 4 cycles"),
                "packed_insts": (k.get("packed") or {}).get("total"),
                "packed": k.get("packed"),
                "sq_insts_valu_f64": sum(pmc.get(c, 0.0) for c in F64_COUNTERS) if any(
