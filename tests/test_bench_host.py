@@ -155,3 +155,22 @@ def test_roofline_block_prices_the_committed_pmc(n_fft):
     assert 0.3 < r["frac"] < 1.0
     assert all("GBps" not in k or (r[k] or 0) < 8000 for k in r)
     json.dumps(r)  # the line must serialise
+
+
+def test_valu_prices_match_the_committed_calibration():
+    """bench.py's per-kind VALU prices are the chip-wide micro-benchmark's
+    (profiles/r06_micro_valu_cal.json, tools/micro/valu_cal.hip and
+    valu_mix.hip, 8 waves/SIMD): packed f32 and fp64 at 4, a transcendental at
+    8 (within 10 %), and the scalar f32 price 2 no higher than what the
+    dual-issuing mixes reach (2.3-2.5) — a lower bound on scalar cost."""
+    import json
+    path = os.path.join(bench.REPO, "profiles", "r06_micro_valu_cal.json")
+    cal = json.load(open(path))
+    s = cal["summary_8_waves"]
+    assert abs(s["v_pk_fma_f32"]["cycles_per_wave_inst_8w"] / bench.PK_CYC - 1) < 0.1
+    assert abs(s["v_exp_f32"]["cycles_per_wave_inst_8w"] / bench.TRANS_CYC - 1) < 0.1
+    assert abs(s["v_fma_f64"]["cycles_per_wave_inst_8w"] / bench.F64_CYC - 1) < 0.15
+    mix = cal["mix"]
+    assert bench.VALU_CYC <= min(mix["v_add_f32 + v_add_f32"]["8"], mix["v_fma_f32(vvv) + v_add_f32"]["8"])
+    # the FP32 peak needs packed math: a scalar FMA stream reaches about half
+    assert s["v_pk_fma_f32"]["tflops_8w"] > 1.8 * s["v_fma_f32"]["tflops_8w"]
