@@ -169,6 +169,36 @@ def test_gain_matrices_match_oracle_gains():
         assert np.max(np.abs(Gd - ref)) < 1e-4, alg
 
 
+def test_bin_m2_by_one_wave_matches_the_per_lane_form():
+    """The sweep kernels evaluate bin M/2 of every cell in one wave per frame
+    (cse_enhance.hip WG::M2C, r06); the gain-writing kernels (want_gains) keep
+    the per-lane form.  Same cells through both: waveforms and SNR sums agree
+    to rounding (the same arithmetic on the same row values; printed whether
+    bit for bit), every algorithm, both n_fft, every frame parity, lag 0."""
+    import torch
+    from classical_speech_enhancement_amd.engine import Engine
+    clean, noisy = make_pair(6, seconds=1.3)
+    eng = Engine()
+    x = torch.as_tensor(noisy).cuda().view(1, -1)
+    c = torch.as_tensor(clean).cuda().view(1, -1)
+    specs = []
+    for n_fft, hop in ((512, 128), (512, 256), (1024, 256), (1024, 128)):
+        for alg in ("ss", "wiener", "mmse", "omlsa"):
+            name = {"ss": "spectralSubtractor"}.get(alg, alg)
+            specs.append((0, name, dict(CELLS[alg], n_fft=n_fft, hop_length=hop, noise_percentile=20.0,
+                                        noise_method="min_tracking")))
+    a = eng.run(x, specs, clean=c, want_waveforms=True)
+    b = eng.run(x, specs, clean=c, want_waveforms=True, want_gains=True)
+    ya, yb = a["y"].double().cpu().numpy(), b["y"].double().cpu().numpy()
+    same = [bool(np.array_equal(ya[j], yb[j])) for j in range(len(specs))]
+    print("bit-identical waveforms:", sum(same), "of", len(specs))
+    for j, (_, alg, p) in enumerate(specs):
+        scale = np.max(np.abs(yb[j]))
+        assert np.max(np.abs(ya[j] - yb[j])) <= 1e-6 * scale, (alg, p["n_fft"], p["hop_length"])
+        assert abs(a["sse"][j] - b["sse"][j]) <= 1e-6 * b["sse"][j], (alg, p["n_fft"])
+    assert a["finite"].all() and b["finite"].all()
+
+
 @pytest.mark.parametrize("v_max", [5.0, 20.0, 80.0, 150.0])
 def test_omlsa_v_max_against_oracle(P, v_max):
     """OMLSA's v_max (advanced_mmse.py signature default 80, not swept by the
