@@ -250,6 +250,57 @@ def rank_job(args, world, rank, n_fft):
     return pair_ids, local, gids, units, total_pairs
 
 
+class ClockSampler:
+    """The shader clock's DPM level while the timed steps run: sysfs
+    pp_dpm_sclk (the level marked '*'), read every 50 ms on a thread, so a line
+    from a box that held a lower clock says so (the level is what the power
+    manager selected; a power-capped part may run below it).  Empty where sysfs
+    is not readable."""
+
+    def __init__(self, period=0.05):
+        import glob
+        import threading
+        self.files = sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk"))
+        self.period, self.samples = period, []
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, daemon=True)
+
+    def _read(self):
+        import re
+        best = None
+        for f in self.files:
+            try:
+                for line in open(f):
+                    if "*" in line:
+                        m = re.search(r"(\d+)\s*[Mm][Hh]z", line)
+                        if m:
+                            best = max(best or 0, int(m.group(1)))
+            except OSError:
+                pass
+        return best
+
+    def _run(self):
+        while not self._stop.is_set():
+            v = self._read()
+            if v is not None:
+                self.samples.append(v)
+            self._stop.wait(self.period)
+
+    def start(self):
+        if self.files:
+            self._thread.start()
+        return self
+
+    def stop(self):
+        if self.files:
+            self._stop.set()
+            self._thread.join()
+        x = self.samples
+        return {"source": "sysfs pp_dpm_sclk (DPM level, every 50 ms during the timed steps)",
+                "n": len(x), "mean_mhz": (sum(x) / len(x)) if x else None,
+                "min_mhz": min(x) if x else None, "max_mhz": max(x) if x else None}
+
+
 class TimedJob:
     """A rank's share of one step's work — STFT + noise PSDs, the fused enhance
     of every cell (one launch per n_fft), one all_gather of the per-cell records
@@ -422,11 +473,13 @@ class TimedJob:
         if self.dist is not None:
             self.dist.barrier()
         torch.cuda.synchronize()
+        clock = ClockSampler().start()
         t0 = time.perf_counter()
         for k in range(steps):
             self.step(evs[k])
         torch.cuda.synchronize()
         local = time.perf_counter() - t0
+        self.clock = clock.stop()
         if self.dist is not None:
             self.dist.barrier()
         dt = time.perf_counter() - t0
@@ -544,6 +597,7 @@ def main():
     units = job.units
     dt, kern = job.run(args.steps, args.warmup)
     kern_ms = kern[0]
+    clock = job.clock
     ranks = gather_rank_stats(dict(job.rank_stats, pairs=len(pair_ids)), dist_ctx)
     n_cells_job = len(grid_specs(1, args.nfft)) * total_pairs
     table = job.table(n_cells_job)
@@ -643,6 +697,7 @@ def main():
             "finalize_alignment": bool(args.align),
         },
         "roofline": roofline_block(args.nfft, units, kern_ms),
+        "clock": clock,
         "ranks": ranks,
     }
     if full is not None:
