@@ -258,12 +258,40 @@ class ClockSampler:
     is not readable."""
 
     def __init__(self, period=0.05):
-        import glob
         import threading
-        self.files = sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk"))
+        self.files = self._card_files()
         self.period, self.samples = period, []
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._run, daemon=True)
+
+    @staticmethod
+    def _card_files():
+        """pp_dpm_sclk of the GPU this process uses (the host's sysfs lists
+        every card): matched by PCI bus id, from torch's device properties or
+        hipDeviceGetPCIBusId of the HIP runtime already loaded; [] if unknown."""
+        import ctypes
+        import glob
+        try:
+            import torch
+            dev = torch.cuda.current_device()
+            bus = None
+            prop = torch.cuda.get_device_properties(dev)
+            if getattr(prop, "pci_bus_id", None) is not None:
+                bus = "%02x:%02x" % (prop.pci_bus_id, getattr(prop, "pci_device_id", 0))
+            if bus is None:
+                lib = next((line.split()[-1] for line in open("/proc/self/maps")
+                            if "libamdhip64.so" in line), None)
+                if lib:
+                    buf = ctypes.create_string_buffer(64)
+                    if ctypes.CDLL(lib).hipDeviceGetPCIBusId(buf, 64, dev) == 0:
+                        bus = buf.value.decode().lower().split(":", 1)[-1].rsplit(".", 1)[0]
+            if bus:
+                import os as _os
+                return [f + "/pp_dpm_sclk" for f in sorted(glob.glob("/sys/class/drm/card*/device"))
+                        if _os.path.basename(_os.path.realpath(f)).lower().rsplit(".", 1)[0].endswith(bus)]
+        except Exception:
+            pass
+        return []
 
     def _read(self):
         import re
@@ -296,7 +324,8 @@ class ClockSampler:
             self._stop.set()
             self._thread.join()
         x = self.samples
-        return {"source": "sysfs pp_dpm_sclk (DPM level, every 50 ms during the timed steps)",
+        return {"source": ("sysfs pp_dpm_sclk of this process's GPU (DPM level, every 50 ms during "
+                           "the timed steps)"), "files": self.files,
                 "n": len(x), "mean_mhz": (sum(x) / len(x)) if x else None,
                 "min_mhz": min(x) if x else None, "max_mhz": max(x) if x else None}
 
