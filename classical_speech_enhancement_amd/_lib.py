@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("CSE_LIB", os.path.join(HERE, "libcse.so"))
 CSE_OK = 0
 # ABI revision this package mirrors (cse_version(); CELL_DTYPE == cse_cell_t,
 # NOISE_JOB_DTYPE == cse_noise_job_t, NoiseParams == cse_noise_params_t)
-ABI_VERSION = 4
+ABI_VERSION = 5
 ALGO = {"NONE": -1, "SS": 0, "WIENER": 1, "MMSE": 2, "OMLSA": 3}
 NOISE = {"percentile": 0, "min_tracking": 1, "true_noise": 2}
 
@@ -50,7 +50,7 @@ EXPORTS = ("cse_version", "cse_last_error", "cse_cells_per_group", "cse_stft",
            "cse_noise_workspace_bytes", "cse_noise_default_params", "cse_noise_estimate_ex",
            "cse_noise_estimate", "cse_noise_smooth", "cse_noise_median",
            "cse_noise_percentile_med", "cse_noise_percentile_med2", "cse_noise_percentile_quad", "cse_noise_min_tracking_med", "cse_noise_finish",
-           "cse_noise_invert", "cse_istft_norm", "cse_enhance_cells",
+           "cse_noise_invert", "cse_istft_norm", "cse_enhance_cells", "cse_enhance_cells_short_hop",
            "cse_xcorr_workspace_bytes", "cse_xcorr_prepare", "cse_xcorr_lag",
            "cse_stoi_workspace_bytes", "cse_stoi_scratch_bytes", "cse_stoi_prepare",
            "cse_stoi_cells")
@@ -133,6 +133,8 @@ def load(path=LIB_PATH):
     lib.cse_stoi_cells.argtypes = [P, P, P, P, i64, i64, i64, i32, P, P, P, P]
     lib.cse_enhance_cells.restype = i32
     lib.cse_enhance_cells.argtypes = [i32, i64, P, i64, P, P, P, P, i64, P, P, P, P]
+    lib.cse_enhance_cells_short_hop.restype = i32
+    lib.cse_enhance_cells_short_hop.argtypes = [i32, i64, P, i64, P, P, P, P, i64, P, P, P]
     # the kernels read the cell/job tables laid out as this package packs them:
     # refuse a library of another ABI revision.  The packer (engine.pack_waves)
     # takes the slot-group size from the library itself; it must be usable.

@@ -1332,7 +1332,7 @@ __device__ __forceinline__ void run_wg(const Args& a, const cse_cell_t* wcell, i
         // w(n)/(NFFT S(n)) at slot q (compile-time after unrolling); at 1024 S is
         // constant and slot q + 16 is w(n + N/2)/(N S) = 1/(N S) - w(n)/(N S)
         load_win();
-        constexpr float KHALF = (float)(1.0 / (NFFT * (R == 8 ? 3.0 : 1.5)));
+        constexpr float KHALF = (float)(1.0 / (NFFT * (0.375 * R)));  // S = 3R/8 (R >= 4)
         auto win = [&](int q) {
             return (W::HALF_TABLES && q >= 16) ? KHALF - wv[q - 16] : wv[q];
         };
@@ -1489,6 +1489,35 @@ __device__ __forceinline__ void dispatch_algo(const Args& a, const cse_cell_t* w
     }
 }
 
+// One workgroup's slot group at hop H0 or H1: the short-hop kernels' entry
+// (enhance_kernel below spells the same steps out for 128 / 256; routed
+// through this function its code came out different, r06).
+template <int NFFT, bool OUT, int H0, int H1>
+__device__ __forceinline__ void enhance_group(const Args& a) {
+    using W = WG<NFFT, OUT>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t first = (int64_t)wg * W::CPWG;
+    const int64_t left = a.n_cells - first;
+    const int n = (int)(left < W::CPWG ? left : W::CPWG);
+    const cse_cell_t* wcell = a.cells + first;
+    // hop and algorithm of the workgroup = its first cell's (the host packs
+    // so); run_wg rejects slots that do not match them.  A group whose slot 0
+    // names no algorithm or a hop outside this kernel's set rejects every
+    // non-padding slot.
+    const int hop = __builtin_amdgcn_readfirstlane(wcell[0].hop);
+    const int algo = __builtin_amdgcn_readfirstlane(wcell[0].algo);
+    if ((hop != H0 && hop != H1) || algo < CSE_ALGO_SS || algo > CSE_ALGO_OMLSA) {
+        for (int c = threadIdx.x; c < n; c += W::THREADS)
+            if (wcell[c].algo != CSE_ALGO_NONE) reject_cell(a, first + c);
+        return;
+    }
+    if (H0 == H1 || hop == H0)
+        dispatch_algo<NFFT, H0, OUT>(a, wcell, n, algo, smem);
+    else
+        dispatch_algo<NFFT, H1, OUT>(a, wcell, n, algo, smem);
+}
+
 // OUT: the g_out (gain matrix) variant for parity tests; waveform output
 // (y_out, any out_len) is available in both variants at run time.
 template <int NFFT, bool OUT>
@@ -1520,11 +1549,32 @@ __global__ void __launch_bounds__(WG<NFFT>::THREADS, CSE_WAVES_PER_SIMD)
         dispatch_algo<NFFT, 256, OUT>(a, wcell, n, algo, smem);
 }
 
+// The short hops (cse_enhance_cells_short_hop): n_fft 512 at hop 32 / 64, n_fft
+// 1024 at hop 64 (a lane retires F = 2 HOP / SP >= 2 samples per frame), no
+// gain-matrix variant.  Kernels of their own, so the sweep kernel above keeps
+// its registers and code.
+template <int NFFT>
+__global__ void __launch_bounds__(WG<NFFT>::THREADS, CSE_WAVES_PER_SIMD)
+    enhance_kernel_short_hop(Args a) {
+    enhance_group<NFFT, false, NFFT == 512 ? 32 : 64, 64>(a);
+}
+
 // The two n_fft halves can be compiled as separate translation units (with
 // their own code-generation flags): cse_enhance_512.hip defines
 // CSE_ENHANCE_ONLY=512 and holds the 512 kernels, cse_enhance_1024.hip the
-// 1024 kernels and the C entry points.  Compiled on its own (analysis tools),
-// this file holds everything.
+// 1024 kernels and the C entry points.  The short-hop kernels are a unit of
+// their own (cse_enhance_short.hip defines CSE_ENHANCE_SHORT): instantiated
+// beside the sweep kernels they moved the compiler's inlining of the shared
+// helpers, and the sweep kernels' code with it.  Compiled on its own
+// (analysis tools), this file holds everything.
+#if defined(CSE_ENHANCE_SHORT) || !defined(CSE_ENHANCE_ONLY)
+const void* enhance_fn_512_short_hop() { return (const void*)enhance_kernel_short_hop<512>; }
+const void* enhance_fn_1024_short_hop() { return (const void*)enhance_kernel_short_hop<1024>; }
+#else
+const void* enhance_fn_512_short_hop();   // cse_enhance_short.hip
+const void* enhance_fn_1024_short_hop();
+#endif
+#ifndef CSE_ENHANCE_SHORT
 #if !defined(CSE_ENHANCE_ONLY) || CSE_ENHANCE_ONLY == 512
 const void* enhance_fn_512(bool out) {
     return out ? (const void*)enhance_kernel<512, true> : (const void*)enhance_kernel<512, false>;
@@ -1538,10 +1588,11 @@ const void* enhance_fn_1024(bool out) {
 #if defined(CSE_ENHANCE_ONLY) && CSE_ENHANCE_ONLY == 1024
 const void* enhance_fn_512(bool out);  // cse_enhance_512.hip
 #endif
+#endif  // !CSE_ENHANCE_SHORT
 
 }  // namespace cse
 
-#ifdef CSE_ENH_STAMPS
+#if defined(CSE_ENH_STAMPS) && !defined(CSE_ENHANCE_SHORT)
 // analysis builds only: per-workgroup stage cycles into buf [n_groups][10]
 // (u64: 8 stages, algorithm, hop) of this translation unit's n_fft, or off (NULL)
 #if !defined(CSE_ENHANCE_ONLY) || CSE_ENHANCE_ONLY == 512
@@ -1555,27 +1606,30 @@ extern "C" int cse_enhance_stamp_buffer_1024(void* buf) {
 }
 #endif
 
-#if !defined(CSE_ENHANCE_ONLY) || CSE_ENHANCE_ONLY == 1024
+#if !defined(CSE_ENHANCE_SHORT) && (!defined(CSE_ENHANCE_ONLY) || CSE_ENHANCE_ONLY == 1024)
 using namespace cse;
 
 extern "C" int cse_cells_per_group(int n_fft) {
     return (n_fft == 512 || n_fft == 1024) ? CSE_CELLS_PER_GROUP(n_fft) : 0;
 }
 
-extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
-                                 const float* Y, const float* noise, const double* clean,
-                                 float* y_out, int64_t out_len, float* g_out, double* sse,
-                                 uint8_t* finite, cse_stream_t stream) {
-    CSE_CHECK_ARG(n_fft == 512 || n_fft == 1024, "cse_enhance_cells: n_fft=%d (512|1024)", n_fft);
-    CSE_CHECK_ARG(cells && Y && noise, "cse_enhance_cells: NULL cells/Y/noise");
-    CSE_CHECK_ARG(len >= 1 && len < (1ll << 30) && n_cells >= 0,
-                  "cse_enhance_cells: len=%lld n_cells=%lld", (long long)len, (long long)n_cells);
+// cse_enhance_cells / cse_enhance_cells_short_hop: one launch over the cells
+static int enhance_launch(const char* name, bool short_hop, int n_fft, int64_t len,
+                          const cse_cell_t* cells, int64_t n_cells, const float* Y,
+                          const float* noise, const double* clean, float* y_out, int64_t out_len,
+                          float* g_out, double* sse, uint8_t* finite, cse_stream_t stream) {
+    CSE_CHECK_ARG(n_fft == 512 || n_fft == 1024, "%s: n_fft=%d (512|1024)", name, n_fft);
+    CSE_CHECK_ARG(cells && Y && noise, "%s: NULL cells/Y/noise", name);
+    CSE_CHECK_ARG(len >= 1 && len < (1ll << 30) && n_cells >= 0, "%s: len=%lld n_cells=%lld", name,
+                  (long long)len, (long long)n_cells);
     // n_fft 512 reads its rows through buffer resources with 32-bit byte
     // offsets (run_wg's ROWS_BUF): the signal's spectrum rows at the smallest hop
     // must stay below 2 GiB
-    CSE_CHECK_ARG(n_fft != 512 || (1 + len / 128) * 257 * 8 < (1ll << 31),
-                  "cse_enhance_cells: len=%lld too long for n_fft=512 (spectrum rows >= 2 GiB)",
+    const int64_t min_hop = short_hop ? 32 : 128;
+    CSE_CHECK_ARG(n_fft != 512 || (1 + len / min_hop) * 257 * 8 < (1ll << 31),
+                  "%s: len=%lld too long for n_fft=512 (spectrum rows >= 2 GiB)", name,
                   (long long)len);
+    CSE_CHECK_ARG(!short_hop || !g_out, "%s: no gain-matrix output at the short hops", name);
     if (n_cells == 0) return CSE_OK;
     Args a;
     a.len = len;
@@ -1591,32 +1645,48 @@ extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells
     a.finite = finite;
     const int per = CSE_CELLS_PER_GROUP(n_fft);
     const int64_t groups = (n_cells + per - 1) / per;
-    CSE_CHECK_ARG(groups < (1ll << 31), "cse_enhance_cells: too many cells");
-    CSE_CHECK_ARG(!y_out || (out_len >= 0 && out_len <= len),
-                  "cse_enhance_cells: out_len=%lld not in [0, len]", (long long)out_len);
+    CSE_CHECK_ARG(groups < (1ll << 31), "%s: too many cells", name);
+    CSE_CHECK_ARG(!y_out || (out_len >= 0 && out_len <= len), "%s: out_len=%lld not in [0, len]",
+                  name, (long long)out_len);
     const bool out = g_out != nullptr;  // the gain-writing variant
     const void* fn;
     int bytes, threads;
     if (n_fft == 512) {
-        fn = enhance_fn_512(out);
+        fn = short_hop ? enhance_fn_512_short_hop() : enhance_fn_512(out);
         bytes = out ? WG<512, true>::BYTES : WG<512, false>::BYTES;
         threads = WG<512>::THREADS;
     } else {
-        fn = enhance_fn_1024(out);
+        fn = short_hop ? enhance_fn_1024_short_hop() : enhance_fn_1024(out);
         bytes = out ? WG<1024, true>::BYTES : WG<1024, false>::BYTES;
         threads = WG<1024>::THREADS;
     }
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) {
-        ::cse::set_error("cse_enhance_cells: cannot reserve %d bytes of LDS", bytes);
+        ::cse::set_error("%s: cannot reserve %d bytes of LDS", name, bytes);
         return CSE_ELAUNCH;
     }
     void* args[] = {&a};
     if (hipLaunchKernel(fn, dim3((unsigned)groups), dim3(threads), args, (size_t)bytes,
                         (hipStream_t)stream) != hipSuccess) {
-        ::cse::set_error("cse_enhance_cells: launch failed");
+        ::cse::set_error("%s: launch failed", name);
         return CSE_ELAUNCH;
     }
-    CSE_CHECK_LAUNCH("cse_enhance_cells");
+    CSE_CHECK_LAUNCH(name);
     return CSE_OK;
+}
+
+extern "C" int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
+                                 const float* Y, const float* noise, const double* clean,
+                                 float* y_out, int64_t out_len, float* g_out, double* sse,
+                                 uint8_t* finite, cse_stream_t stream) {
+    return enhance_launch("cse_enhance_cells", false, n_fft, len, cells, n_cells, Y, noise, clean,
+                          y_out, out_len, g_out, sse, finite, stream);
+}
+
+extern "C" int cse_enhance_cells_short_hop(int n_fft, int64_t len, const cse_cell_t* cells,
+                                           int64_t n_cells, const float* Y, const float* noise,
+                                           const double* clean, float* y_out, int64_t out_len,
+                                           double* sse, uint8_t* finite, cse_stream_t stream) {
+    return enhance_launch("cse_enhance_cells_short_hop", true, n_fft, len, cells, n_cells, Y,
+                          noise, clean, y_out, out_len, nullptr, sse, finite, stream);
 }
 #endif  // the C entry points

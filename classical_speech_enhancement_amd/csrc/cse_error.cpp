@@ -16,4 +16,4 @@ void set_error(const char* fmt, ...) {
 }  // namespace cse
 
 extern "C" const char* cse_last_error(void) { return cse::g_err; }
-extern "C" int cse_version(void) { return 4; }
+extern "C" int cse_version(void) { return 5; }

@@ -54,6 +54,17 @@ def _ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+def _at(t, k):
+    """Pointer to element k of a device tensor (None stays None)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr() + k * t.element_size())
+
+
+# hops of the sweep kernels (cse_enhance_cells) and the short hops of
+# cse_enhance_cells_short_hop, per n_fft
+HOPS = (128, 256)
+SHORT_HOPS = {512: (32, 64), 1024: (64,)}
+
+
 def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
@@ -382,6 +393,7 @@ class GridPlan:
         self.cells = cells
         packed, self.order = pack_waves(cells, n_fft)
         self.n_packed = len(packed)
+        self.n_main = main_slots(packed)
         self.cells_d = torch.from_numpy(packed.view(np.uint8).copy()).to(dev)
         self.g_out = torch.zeros(max(g_total, 1), dtype=torch.float32, device=dev) if want_g else None
         self.y_all = y_all
@@ -405,6 +417,7 @@ class GridPlan:
                 head_off = np.arange(len(items), dtype=np.int64) * self.xc_n
                 self.cells["out_offset"] = head_off
                 packed, _ = pack_waves(self.cells, n_fft)
+                assert main_slots(packed) == self.n_main
                 self.cells_d = torch.from_numpy(packed.view(np.uint8).copy()).to(dev)
             self.head_off = torch.as_tensor(head_off, device=dev)
             self.sig_of = torch.as_tensor(sig.astype(np.int32), device=dev)
@@ -520,11 +533,21 @@ class GridPlan:
             yo, olen = self.head, self.xc_n
         else:
             yo, olen = None, 0
-        _lib.check(self.lib.cse_enhance_cells(
-            self.n_fft, self.L, _ptr(self.cells_d), self.n_packed, _ptr(self.Ybuf),
-            _ptr(self.pool), _ptr(self.clean), _ptr(yo), olen, _ptr(self.g_out),
-            _ptr(self.sse_d), _ptr(self.fin_d), _stream()),
-            "cse_enhance_cells")
+        self.launch(self.cells_d, self.n_packed, self.n_main, yo, olen, self.g_out, self.sse_d,
+                    self.fin_d, _stream(), "cse_enhance_cells")
+
+    def launch(self, cells_d, n, n_main, yo, olen, g, sse, fin, st, what):
+        """The enhance launches over packed cells: slots [0, n_main) at the
+        sweep hops (cse_enhance_cells, one kernel), the rest at the short hops
+        (cse_enhance_cells_short_hop; pack_waves puts those groups last)."""
+        args = (_ptr(self.Ybuf), _ptr(self.pool), _ptr(self.clean), _ptr(yo), olen)
+        if n_main:
+            _lib.check(self.lib.cse_enhance_cells(self.n_fft, self.L, _ptr(cells_d), n_main, *args,
+                                                  _ptr(g), _ptr(sse), _ptr(fin), st), what)
+        if n > n_main:
+            _lib.check(self.lib.cse_enhance_cells_short_hop(
+                self.n_fft, self.L, _at(cells_d, n_main * _lib.CELL_DTYPE.itemsize), n - n_main,
+                *args, _at(sse, n_main), _at(fin, n_main), st), what + "(short hop)")
 
     def execute(self, noisy, clean=None):
         self.prepare(noisy, clean)
@@ -558,10 +581,8 @@ class GridPlan:
         cd = torch.from_numpy(packed.view(np.uint8).copy()).to(self.device)
         sse = torch.zeros(len(packed), dtype=torch.float64, device=self.device)
         fin = torch.zeros(len(packed), dtype=torch.uint8, device=self.device)
-        _lib.check(lib.cse_enhance_cells(
-            self.n_fft, self.L, _ptr(cd), len(packed), _ptr(self.Ybuf), _ptr(self.pool),
-            _ptr(self.clean), None, 0, None, _ptr(sse), _ptr(fin), st),
-            "cse_enhance_cells(aligned)")
+        self.launch(cd, len(packed), main_slots(packed), None, 0, None, sse, fin, st,
+                    "cse_enhance_cells(aligned)")
         self.rerun = (sel, order, sse, fin)
 
     def results(self):
@@ -610,8 +631,11 @@ class MultiPlan:
                 raise ValueError(f"signal index {sig} out of range")
             ck = (alg, hop, nf, p["noise_method"])
             if ck not in checked:  # per distinct (algorithm, hop, n_fft, method)
-                if hop not in (128, 256) or nf not in (512, 1024):
-                    raise ValueError("engine supports n_fft in {512,1024}, hop in {128,256}")
+                if nf not in (512, 1024) or hop not in HOPS + SHORT_HOPS[nf]:
+                    raise ValueError("engine supports n_fft 512 at hop 32, 64, 128, 256 and "
+                                     "n_fft 1024 at hop 64, 128, 256")
+                if want_g and hop not in HOPS:
+                    raise ValueError(f"gain matrices only at hop in {HOPS}")
                 noise_key(alg, p, n_frames(L, hop))  # validates the method
                 if (p["noise_method"] == "true_noise" and not with_clean
                         and n_frames(L, hop) >= 5):
@@ -703,7 +727,9 @@ def pack_waves(cells, n_fft):
     slot i, or -1 for padding.  Groups are ordered longest-first (frames x
     algorithm cost, then by key) so the launch ends on short workgroups;
     neighbours share rows, and the kernel's XCD remap keeps neighbours on one
-    XCD's L2.  Vectorised (numpy): a 100k-cell table packs in milliseconds.
+    XCD's L2.  Groups at the short hops (SHORT_HOPS) come after all others:
+    they go to a launch of their own (GridPlan.launch, main_slots).
+    Vectorised (numpy): a 100k-cell table packs in milliseconds.
     """
     per = _lib.cells_per_group(n_fft)
     n = len(cells)
@@ -722,7 +748,8 @@ def pack_waves(cells, n_fft):
         if code >= 0:
             cost_of[code] = ALGO_COST[name]
     cost = (1 + 16000 // uniq[:, 0]) * cost_of[uniq[:, 1]]
-    gorder = np.lexsort((np.arange(G), -cost))          # longest first, then key order
+    short = ~np.isin(uniq[:, 0], HOPS)
+    gorder = np.lexsort((np.arange(G), -cost, short))   # longest first, then key order
     slot_base = np.zeros(G, dtype=np.int64)
     slot_base[gorder] = np.concatenate([[0], np.cumsum(nslots[gorder])[:-1]])
     # rank of each cell inside its group, in the cells' original order
@@ -746,6 +773,11 @@ def pack_waves(cells, n_fft):
         packed["out_offset"][pad] = -1
         packed["gain_offset"][pad] = -1
     return packed, order
+
+
+def main_slots(packed):
+    """Packed slots of the sweep-hop groups (pack_waves puts them first)."""
+    return int(np.count_nonzero(np.isin(packed["hop"], HOPS)))
 
 
 def snr_db(sse, clean_power):

@@ -73,7 +73,7 @@ enum {
  */
 typedef struct cse_cell {
     int32_t algo;          /* CSE_ALGO_* */
-    int32_t hop;           /* hop length; 128 or 256 */
+    int32_t hop;           /* hop length; 128 or 256 (short hops: cse_enhance_cells_short_hop) */
     int64_t y_offset;      /* offset (in complex elements) of this cell's spectrum Y[T][B] */
     int64_t noise_offset;  /* offset (floats) of this cell's noise row: the PSD N itself for
                               CSE_ALGO_SS, 1/max(N, eps) (cse_noise_invert) for the others */
@@ -274,6 +274,20 @@ int cse_enhance_cells(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n
                       const float* Y, const float* noise, const double* clean,
                       float* y_out, int64_t out_len, float* g_out, double* sse,
                       uint8_t* finite, cse_stream_t stream);
+
+/*
+ * cse_enhance_cells at the short hops the plugins accept beside the grid's
+ * 128/256 (spectral_subtractor.py:6, wiener_filter.py:7, mmse.py:6,
+ * advanced_mmse.py:7 take any hop_length): n_fft 512 at hop 32 or 64, n_fft
+ * 1024 at hop 64 — kernels of their own, so every slot group of `cells` must
+ * name one of those hops (a group at another hop is rejected as above; the
+ * 128/256 groups go to cse_enhance_cells).  Same cells, rows, outputs and
+ * limits (n_fft 512: (1 + len/32) * 257 * 8 < 2^31), no gain-matrix output.
+ */
+int cse_enhance_cells_short_hop(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
+                                const float* Y, const float* noise, const double* clean,
+                                float* y_out, int64_t out_len, double* sse, uint8_t* finite,
+                                cse_stream_t stream);
 
 /*
  * Alignment of finalize_enhanced (speech_enhancement_comparison.py:38-69, 92-106):

@@ -293,10 +293,43 @@ def gen_presentation(R):
     print("presentation done")
 
 
+SHORT_HOPS = ((512, 32), (512, 64), (1024, 64))
+
+
+def gen_short_hops(R):
+    """Fixture: every algorithm x method at the short hops the plugins accept
+    beyond the grid's 128/256 (cse_enhance_cells_short_hop) on a 0.5-s pair,
+    plus T < 5 and T ~ 10 clips at hop 32.  Outputs stored as float32 (6e-8
+    relative, far inside the 1e-5 tolerance)."""
+    clean, noisy = make_pair(11, seconds=0.5)
+    clean = clean.astype(np.float32).astype(np.float64)
+    out = {"clean": clean.astype(np.float32), "noisy": noisy, "synth": np.asarray([11, 0.5])}
+    for alg, base in CELLS.items():
+        for method in ("percentile", "min_tracking", "true_noise"):
+            for n_fft, hop in SHORT_HOPS:
+                kw = dict(base, n_fft=n_fft, hop_length=hop, noise_percentile=10.0,
+                          noise_method=method)
+                if method == "true_noise":
+                    kw["clean_audio"] = clean
+                y = R[alg](noisy, 16000, **kw)
+                out[f"y|{alg}|{method}|{n_fft}|{hop}"] = np.asarray(y, dtype=np.float32)
+    for n in (100, 300):   # T = 4 (static fallback) and T = 10 at hop 32
+        x = noisy[:n].copy()
+        out[f"noisy|{n}"] = x
+        for alg, base in CELLS.items():
+            y = R[alg](x, 16000, **dict(base, n_fft=512, hop_length=32, noise_percentile=20.0,
+                                        noise_method="min_tracking"))
+            out[f"t|{n}|{alg}"] = np.asarray(y, dtype=np.float32)
+    np.savez_compressed(os.path.join(OUT, "short_hops_0p5s.npz"), **out)
+    print("short_hops_0p5s.npz", len(out))
+
+
 if __name__ == "__main__":
     R = ref_modules()
     which = sys.argv[1:] or ["algorithms", "config1", "short", "presentation", "grid", "tiny",
-                             "noise_params"]
+                             "noise_params", "short_hops"]
+    if "short_hops" in which:
+        gen_short_hops(R)
     if "algorithms" in which:
         gen_algorithms(R)
     if "config1" in which:

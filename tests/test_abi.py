@@ -56,6 +56,36 @@ def test_version_and_error_channel(lib):
         rc = lib.cse_enhance_cells(n_fft, n, ctypes.c_void_p(16), 0, ctypes.c_void_p(16),
                                    ctypes.c_void_p(16), None, None, 0, None, None, None, None)
         assert rc == 0, lib.cse_last_error()
+    # the short hops: rows at hop 32, so (1 + len/32) * 257 * 8 < 2^31 at 512
+    ok32 = ((2**31 - 1) // (257 * 8) - 1) * 32 + 31
+    args = (ctypes.c_void_p(16), 0, ctypes.c_void_p(16), ctypes.c_void_p(16), None, None, 0,
+            None, None, None)
+    rc = lib.cse_enhance_cells_short_hop(256, 100, *args)
+    assert rc == -1 and b"cse_enhance_cells_short_hop: n_fft" in lib.cse_last_error()
+    rc = lib.cse_enhance_cells_short_hop(512, ok32 + 1, *args)
+    assert rc == -1 and b"too long for n_fft=512" in lib.cse_last_error()
+    for n_fft, n in ((512, ok32), (1024, ok32 + 1)):
+        assert lib.cse_enhance_cells_short_hop(n_fft, n, *args) == 0, lib.cse_last_error()
+
+
+def test_short_hop_groups_pack_last():
+    """pack_waves puts the short-hop groups after the sweep-hop ones (their
+    own launch: GridPlan.launch), whatever their cost; main_slots counts the
+    sweep-hop slots."""
+    from classical_speech_enhancement_amd.engine import main_slots, pack_waves
+    cells = np.zeros(9, dtype=_lib.CELL_DTYPE)
+    cells["algo"] = [0, 3, 3, 1, 0, 3, 2, 2, 3]
+    cells["hop"] = [32, 256, 64, 128, 128, 32, 256, 64, 128]
+    cells["y_offset"] = np.arange(9)
+    packed, order = pack_waves(cells, 512)
+    G = _lib.cells_per_group(512)
+    k = main_slots(packed)
+    assert k == 5 * G  # five sweep-hop cells, each its own group (distinct rows)
+    assert set(packed["hop"][:k].tolist()) == {128, 256}
+    assert set(packed["hop"][k:].tolist()) == {32, 64}
+    assert sorted(order[order >= 0].tolist()) == list(range(9))
+    # inside each part: longest first (hop 32 OMLSA leads the short part)
+    assert packed[k]["hop"] == 32 and packed[k]["algo"] == 3
 
 
 def test_cells_per_group_matches_header(lib):

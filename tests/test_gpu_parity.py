@@ -75,6 +75,84 @@ def test_noise_estimates_match_reference_golden(P):
         np.testing.assert_allclose(N, g[key], rtol=1e-6, atol=0, err_msg=key)
 
 
+def test_short_hops_match_reference_golden(P):
+    """cse_enhance_cells_short_hop (n_fft 512 at hop 32 / 64, 1024 at 64)
+    through the plugins against the reference's outputs (float32-stored, 6e-8),
+    incl. T = 4 (static fallback) and T = 10 clips at hop 32."""
+    g = load_golden("short_hops_0p5s.npz")
+    noisy, clean = g["noisy"], g["clean"].astype(np.float64)
+    n = 0
+    for key in g.files:
+        if key.startswith("y|"):
+            alg, method, n_fft, hop = key.split("|")[1:]
+            kw = dict(CELLS[alg], n_fft=int(n_fft), hop_length=int(hop), noise_percentile=10.0,
+                      noise_method=method)
+            if method == "true_noise":
+                kw["clean_audio"] = clean
+            y = _fn(P, alg)(noisy, 16000, **kw)
+        elif key.startswith("t|"):
+            m, alg = key.split("|")[1:]
+            y = _fn(P, alg)(g[f"noisy|{m}"], 16000, **dict(CELLS[alg], n_fft=512, hop_length=32,
+                                                             noise_percentile=20.0,
+                                                             noise_method="min_tracking"))
+        else:
+            continue
+        ref = g[key].astype(np.float64)
+        assert y.shape == ref.shape, key
+        assert rel_l2(y, ref) <= TOL and rel_max(y, ref) <= TOL, (key, rel_l2(y, ref))
+        n += 1
+    assert n == 44
+
+
+def test_short_and_sweep_hops_in_one_plan(P):
+    """One plan mixing sweep-hop and short-hop cells (two launches over one
+    packed table) equals the cells run one plan each (the same cell code; a
+    misplaced output pointer would show as a gross error); gain matrices at a
+    short hop and unsupported hops raise."""
+    import torch
+    from classical_speech_enhancement_amd.engine import Engine
+    clean, noisy = make_pair(5, seconds=0.5)
+    eng = Engine()
+    x = torch.as_tensor(np.stack([noisy, noisy[::-1].copy()])).cuda()
+    c = torch.as_tensor(np.stack([clean, clean[::-1].copy()])).cuda()
+    specs = []
+    for s in (0, 1):
+        for alg, kw in (("wiener", CELLS["wiener"]), ("omlsa", CELLS["omlsa"]),
+                        ("ss", CELLS["ss"]), ("mmse", CELLS["mmse"])):
+            for n_fft, hop in ((512, 128), (512, 32), (1024, 64), (1024, 256), (512, 64)):
+                specs.append((s, alg, dict(kw, n_fft=n_fft, hop_length=hop, noise_percentile=10.0,
+                                           noise_method="min_tracking")))
+    together = eng.run(x, specs, clean=c, want_waveforms=True)
+    yt = together["y"].cpu().numpy()
+    for i, sp in enumerate(specs):
+        alone = eng.run(x, [sp], clean=c, want_waveforms=True)
+        ya = alone["y"][0].cpu().numpy()
+        assert rel_max(yt[i], ya) <= 1e-6, sp
+        assert abs(together["sse"][i] - alone["sse"][0]) <= 1e-9 * alone["sse"][0], sp
+        assert together["finite"][i] and alone["finite"][0], sp
+    with pytest.raises(ValueError, match="gain matrices"):
+        eng.run(x, specs[1:2], clean=c, want_gains=True)
+    with pytest.raises(ValueError, match="engine supports"):
+        eng.run(x, [(0, "wiener", dict(CELLS["wiener"], n_fft=1024, hop_length=32,
+                                       noise_percentile=10.0, noise_method="percentile"))])
+
+
+@pytest.mark.parametrize("n_fft,hop", [(512, 32), (512, 64), (1024, 64)])
+def test_short_hops_10s_vs_oracle(P, n_fft, hop):
+    """10-s signals (5001 frames at hop 32) at the short hops, every algorithm,
+    against the fp64 oracle at the north-star tolerance."""
+    clean, noisy = make_pair(3, seconds=10.0)
+    for alg, method in (("ss", "true_noise"), ("wiener", "percentile"),
+                        ("mmse", "min_tracking"), ("omlsa", "min_tracking")):
+        kw = dict(CELLS[alg], n_fft=n_fft, hop_length=hop, noise_percentile=10.0,
+                  noise_method=method)
+        if method == "true_noise":
+            kw["clean_audio"] = clean
+        y = _fn(P, alg)(noisy, 16000, **kw)
+        ref = ORACLE[alg](noisy, 16000, **kw)
+        assert rel_l2(y, ref) <= TOL and rel_max(y, ref) <= TOL, (alg, rel_l2(y, ref))
+
+
 def test_config1_ss_true_noise_10s(P):
     g = load_golden("config1_ss_true_noise_10s.npz")
     clean, noisy = make_pair(0, seconds=10.0)

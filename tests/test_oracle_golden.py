@@ -72,6 +72,33 @@ def test_noise_estimates_match_reference():
     assert n >= 12
 
 
+def test_short_hops_match_reference():
+    """The short hops (n_fft 512 at 32 / 64, 1024 at 64) and T < 5 / T = 10
+    clips at hop 32; the fixture holds float32 outputs (6e-8 relative)."""
+    g = load_golden("short_hops_0p5s.npz")
+    noisy, clean = g["noisy"], g["clean"].astype(np.float64)
+    n = 0
+    for key in g.files:
+        if key.startswith("y|"):
+            alg, method, n_fft, hop = key.split("|")[1:]
+            kw = dict(CELLS[alg], n_fft=int(n_fft), hop_length=int(hop), noise_percentile=10.0,
+                      noise_method=method)
+            if method == "true_noise":
+                kw["clean_audio"] = clean
+            y = ALG[alg](noisy, 16000, **kw)
+        elif key.startswith("t|"):
+            m, alg = key.split("|")[1:]
+            y = ALG[alg](g[f"noisy|{m}"], 16000, **dict(CELLS[alg], n_fft=512, hop_length=32,
+                                                          noise_percentile=20.0,
+                                                          noise_method="min_tracking"))
+        else:
+            continue
+        assert y.shape == g[key].shape, key
+        assert rel_l2(y, g[key]) < 1e-6 and rel_max(y, g[key]) < 1e-6, key
+        n += 1
+    assert n == 4 * 3 * 3 + 2 * 4
+
+
 def test_config1_ss_true_noise():
     g = load_golden("config1_ss_true_noise_10s.npz")
     clean, noisy = make_pair(0, seconds=10.0)

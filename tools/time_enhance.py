@@ -2,6 +2,10 @@
 timing-only variant builds whose outputs are wrong by construction.
 
     CSE_LIB=... python tools/time_enhance.py [--pairs 13 --nfft 512 --reps 5]
+                                             [--hop-map 128:32,256:64]
+
+--hop-map moves the grid's cells to other hops (here the short hops of
+cse_enhance_cells_short_hop); the line then also gives frame-gain evals/s.
 """
 import argparse
 import json
@@ -18,7 +22,9 @@ def main():
     ap.add_argument("--pairs", type=int, default=13)
     ap.add_argument("--nfft", type=int, default=512)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--hop-map", default="")
     a = ap.parse_args()
+    hop_map = dict(tuple(int(v) for v in kv.split(":")) for kv in a.hop_map.split(",") if kv)
     import torch
     from classical_speech_enhancement_amd.engine import Engine
     from classical_speech_enhancement_amd.parameter_ranges import grid_specs
@@ -26,7 +32,9 @@ def main():
     pairs = [make_pair(i, 10.0) for i in range(a.pairs)]
     clean = torch.as_tensor(np.stack([c for c, _ in pairs])).cuda()
     noisy = torch.as_tensor(np.stack([n for _, n in pairs])).cuda()
-    plan = Engine().plan(a.pairs, 160000, grid_specs(a.pairs, a.nfft), with_clean=True).plans[0]
+    specs = [(s, alg, dict(p, hop_length=hop_map.get(p["hop_length"], p["hop_length"])))
+             for (s, alg, p) in grid_specs(a.pairs, a.nfft)]
+    plan = Engine().plan(a.pairs, 160000, specs, with_clean=True).plans[0]
     plan.prepare(noisy, clean)
     plan.enhance()
     torch.cuda.synchronize()
@@ -38,7 +46,10 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1))
-    print(json.dumps({"lib": os.environ.get("CSE_LIB", "libcse.so"), "kernel_ms": float(np.median(ms))}))
+    med = float(np.median(ms))
+    print(json.dumps({"lib": os.environ.get("CSE_LIB", "libcse.so"), "n_fft": a.nfft,
+                      "hop_map": hop_map, "kernel_ms": med, "units": plan.units,
+                      "evals_per_s": plan.units / (med * 1e-3)}))
 
 
 if __name__ == "__main__":
