@@ -53,7 +53,8 @@ EXPORTS = ("cse_version", "cse_last_error", "cse_cells_per_group", "cse_stft",
            "cse_noise_invert", "cse_istft_norm", "cse_enhance_cells", "cse_enhance_cells_short_hop",
            "cse_xcorr_workspace_bytes", "cse_xcorr_prepare", "cse_xcorr_lag",
            "cse_stoi_workspace_bytes", "cse_stoi_scratch_bytes", "cse_stoi_prepare",
-           "cse_stoi_cells")
+           "cse_stoi_cells", "cse_stoi_workspace_bytes_sr", "cse_stoi_scratch_bytes_sr",
+           "cse_stoi_cells_sr")
 XCORR_OK, XCORR_FLAT, XCORR_NONFINITE = 0, 1, 2  # FLAT: slow exact path ran (lag exact)
 
 
@@ -131,6 +132,12 @@ def load(path=LIB_PATH):
     lib.cse_stoi_prepare.argtypes = [P, i64, i64, i32, P, P]
     lib.cse_stoi_cells.restype = i32
     lib.cse_stoi_cells.argtypes = [P, P, P, P, i64, i64, i64, i32, P, P, P, P]
+    lib.cse_stoi_workspace_bytes_sr.restype = i64
+    lib.cse_stoi_workspace_bytes_sr.argtypes = [i64, i64, i32]
+    lib.cse_stoi_scratch_bytes_sr.restype = i64
+    lib.cse_stoi_scratch_bytes_sr.argtypes = [i64, i64, i32]
+    lib.cse_stoi_cells_sr.restype = i32
+    lib.cse_stoi_cells_sr.argtypes = [P, P, P, P, i64, i64, i64, i32, i32, P, P, P, P]
     lib.cse_enhance_cells.restype = i32
     lib.cse_enhance_cells.argtypes = [i32, i64, P, i64, P, P, P, P, i64, P, P, P, P]
     lib.cse_enhance_cells_short_hop.restype = i32

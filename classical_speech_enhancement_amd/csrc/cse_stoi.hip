@@ -41,6 +41,8 @@
 // outputs themselves are f32 (the enhance kernel's output type).
 #include "cse_common.hpp"
 
+#include <math.h>
+#include <numeric>
 #include <type_traits>
 
 namespace cse {
@@ -88,17 +90,58 @@ __constant__ int BAND_EDGE[NBAND + 1] = {7, 9, 11, 14, 17, 22, 27, 34, 43, 55,
                                          69, 87, 109, 138, 174, 219};
 }  // namespace stoi
 
+constexpr int stoi_fs10 = 10000;  // pystoi's working rate
+
 struct StoiLayout {
     int64_t n10, F, Mmax, Jmax, NBLK;
-    int64_t coef64, meta, x10, en, kf, btab, xtob, xstat, total;
+    int64_t coef64, meta, x10, en, kf, btab, xtob, xstat, hgen, total;
 };
 
 static inline int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
-static StoiLayout stoi_layout(int64_t n_sig, int64_t len) {
+// Input rates other than 16 kHz: pystoi resamples any fs_sig != 10 kHz with
+// utils.resample_oct(x, 10000, fs_sig), scipy's resample_poly(x, up, down)
+// with Octave's Kaiser window normalised to unit sum (oracle/stoi_ref.py
+// resample_oct).  The filter and resample_poly's padding, per rate:
+struct Resamp {
+    int up, down;             // 10000 / sr reduced; 1 / 1 at 10 kHz (no resampling)
+    int64_t half;             // window half length L: 2L + 1 taps
+    int64_t pre_pad, pre_rm;  // resample_poly's leading zero taps and dropped outputs
+    int64_t n_out;            // ceil(len up / down)
+};
+
+static Resamp resamp_for(int sr, int64_t len) {
+    Resamp r;
+    if (sr == stoi_fs10) {
+        r.up = r.down = 1;
+        r.half = r.pre_pad = r.pre_rm = 0;
+        r.n_out = len;
+        return r;
+    }
+    const int g = std::gcd(stoi_fs10, sr);
+    r.up = stoi_fs10 / g;
+    r.down = sr / g;
+    // _resample_window_oct: stopband 1/(2 max(p, q)), roll-off a tenth of it,
+    // L = ceil((60 - 8) / (28.714 roll-off)) (rejection 60 dB)
+    const double stop = 1.0 / (2.0 * (double)(r.up > r.down ? r.up : r.down));
+    r.half = (int64_t)ceil((60.0 - 8.0) / (28.714 * (stop / 10.0)));
+    r.n_out = (len * r.up + r.down - 1) / r.down;
+    r.pre_pad = r.down - r.half % r.down;
+    r.pre_rm = (r.half + r.pre_pad) / r.down;
+    return r;
+}
+
+static StoiLayout stoi_layout(int64_t n_sig, int64_t len, int sr = 16000) {
     using namespace stoi;
     StoiLayout L;
-    L.n10 = (len * UP + DOWN - 1) / DOWN;  // resample_poly: ceil(len * up / down)
+    int64_t ntap = 0;  // the generic filter (other rates)
+    if (sr == 16000) {
+        L.n10 = (len * UP + DOWN - 1) / DOWN;  // resample_poly: ceil(len * up / down)
+    } else {
+        const Resamp r = resamp_for(sr, len);
+        L.n10 = r.n_out;
+        ntap = 2 * r.half + 1;
+    }
     L.F = L.n10 >= FR ? (L.n10 - FR) / HOP + 1 : 0;
     L.Mmax = L.F > 1 ? L.F - 1 : 0;
     L.Jmax = L.Mmax >= NSEG ? L.Mmax - NSEG + 1 : 0;
@@ -112,6 +155,7 @@ static StoiLayout stoi_layout(int64_t n_sig, int64_t len) {
     L.btab = o;   o = align256(o + n_sig * L.NBLK * BT * 4);
     L.xtob = o;   o = align256(o + n_sig * L.Mmax * 16 * 8);
     L.xstat = o;  o = align256(o + n_sig * L.Jmax * 16 * 32);
+    L.hgen = o;   o = align256(o + ntap * 8);
     L.total = o;
     return L;
 }
@@ -188,6 +232,90 @@ __global__ void __launch_bounds__(256) stoi_resample_clean_kernel(const double* 
 #pragma unroll
     for (int r = 0; r < 5; ++r)
         if (5 * q + r < n10) o[5 * q + r] = acc[r];
+}
+
+// Other input rates, prepare: the normalised Octave filter times up (what
+// resample_poly multiplies the supplied window by), 2 half + 1 taps
+// (np.kaiser(2L + 1, 0.1102 (60 - 8.7)) x 2 up stop sinc(2 stop t)); half = 0
+// is the 10-kHz identity.
+__global__ void __launch_bounds__(1024) stoi_coef_generic_kernel(double* __restrict__ h,
+                                                                  int64_t half, int up, int down) {
+    __shared__ double red[1024];
+    const int tid = threadIdx.x;
+    if (half == 0) {
+        if (tid == 0) h[0] = 1.0;
+        return;
+    }
+    const int64_t n = 2 * half + 1;
+    const double beta = 0.1102 * (60.0 - 8.7);
+    const double i0b = bessel_i0(beta);
+    const double stop = 1.0 / (2.0 * (double)(up > down ? up : down));
+    double part = 0.0;
+    for (int64_t i = tid; i < n; i += 1024) {
+        const double a = (double)half;  // np.kaiser: alpha = (M - 1) / 2
+        const double u = ((double)i - a) / a;
+        const double kais = bessel_i0(beta * sqrt(fmax(1.0 - u * u, 0.0))) / i0b;
+        const double x = 2.0 * stop * (double)(i - half);
+        const double sinc = (i == half) ? 1.0 : sinpi(x) / (M_PI * x);
+        const double v = kais * (2.0 * up * stop * sinc);
+        h[i] = v;
+        part += v;
+    }
+    red[tid] = part;
+    __syncthreads();
+    for (int s = 512; s > 0; s >>= 1) {
+        if (tid < s) red[tid] += red[tid + s];
+        __syncthreads();
+    }
+    const double total = red[0];
+    for (int64_t i = tid; i < n; i += 1024) h[i] = up * (h[i] / total);
+}
+
+// Other input rates: resample_poly as upfirdn(h padded by pre_pad zeros)
+// with its first pre_rm outputs dropped, out[i] = sum over n of
+// h[(i + pre_rm) down - pre_pad - n up] e[n], fp64, one thread per output.
+// TEST: e[n] = y[off + n - lag] (f32, zero outside [0, len) like
+// cse_stoi_cells, clipped to [-1, 1] if clip); else e = x (f64 clean rows).
+template <bool TEST>
+__global__ void __launch_bounds__(256) stoi_resample_kernel(
+    const double* __restrict__ x, const float* __restrict__ y, const int64_t* __restrict__ y_off,
+    const int32_t* __restrict__ lag, int clip, int64_t len, const double* __restrict__ h,
+    int64_t ntap, int up, int down, int64_t pre_pad, int64_t pre_rm, int64_t n_out,
+    double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t s = blockIdx.y;
+    if (i >= n_out) return;
+    const int64_t base = (i + pre_rm) * down - pre_pad;  // tap index of n = 0
+    // taps j = base - n up in [0, ntap): n in [ceil((base - ntap + 1) / up), floor(base / up)]
+    auto fdiv = [](int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); };
+    int64_t nlo = -fdiv(-(base - ntap + 1), up), nhi = fdiv(base, up);
+    int lg = 0;
+    const float* ys = nullptr;
+    const double* xs = nullptr;
+    if (TEST) {
+        lg = lag ? lag[s] : 0;
+        ys = y + y_off[s];
+        // e[n] = y[n - lag] for n and n - lag in [0, len)
+        nlo = nlo > (int64_t)lg ? nlo : (int64_t)lg;
+        nhi = nhi < len - 1 + lg ? nhi : len - 1 + lg;
+    } else {
+        xs = x + s * len;
+    }
+    nlo = nlo > 0 ? nlo : 0;
+    nhi = nhi < len - 1 ? nhi : len - 1;
+    double acc = 0.0;
+    for (int64_t n = nlo; n <= nhi; ++n) {
+        double e;
+        if (TEST) {
+            float v = ys[n - lg];
+            if (clip) v = fminf(fmaxf(v, -1.0f), 1.0f);
+            e = (double)v;
+        } else {
+            e = xs[n];
+        }
+        acc = fma(h[base - n * up], e, acc);
+    }
+    out[s * n_out + i] = acc;
 }
 
 // MATLAB hanning(256) = scipy hann(258)[1:-1]
@@ -460,13 +588,15 @@ __device__ __forceinline__ void stoi_tables(StoiLds& L) {
     }
 }
 
-// PRE: the 10-kHz signal is given (clean side, fp64 x10); otherwise the 16-kHz
-// cell output is resampled here.
+// PRE: the 10-kHz signal is given (fp64 x10: the clean side, and the cells at
+// input rates other than 16 kHz); otherwise the 16-kHz cell output is
+// resampled here.
 template <bool PRE>
-__device__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t len, int lag,
-                             bool clip, const double* __restrict__ x10,
-                             const double* __restrict__ coef, const int* __restrict__ btab,
-                             int nblk, double* __restrict__ env, StoiStamps& ts) {
+__device__ __forceinline__ void stoi_phase_a(StoiLds& L, const float* __restrict__ y, int64_t len,
+                                             int lag, bool clip, const double* __restrict__ x10,
+                                             const double* __restrict__ coef,
+                                             const int* __restrict__ btab, int nblk,
+                                             double* __restrict__ env, StoiStamps& ts) {
     using namespace stoi;
     const int tid = threadIdx.x;
     // 16-kHz input samples of one staging chunk, loaded into registers one
@@ -764,13 +894,14 @@ struct StoiArgs {
     double* out;
 };
 
-// coef is a separate const __restrict__ argument so the compiler can prove it
-// is never written and read it through the scalar cache (s_load): inside the
-// argument struct it became per-lane vector loads waited on right after issue
-__global__ void __launch_bounds__(stoi::NT, 3) stoi_cells_kernel(StoiArgs a,
-                                                              const double* __restrict__ coef) {
+// PRE: the cell's test signal is given at 10 kHz (y10 + c n10, fp64: other
+// input rates, resampled by stoi_resample_kernel); otherwise the 16-kHz
+// output y is resampled in phase A.
+template <bool PRE>
+__device__ __forceinline__ void stoi_cells_body(StoiLds& L, const StoiArgs& a,
+                                                const double* __restrict__ coef,
+                                                const double* __restrict__ y10, int64_t n10) {
     using namespace stoi;
-    __shared__ StoiLds L;
     const int64_t c = blockIdx.x;
     const int tid = threadIdx.x;
     const int sig = a.sig_of[c];
@@ -788,8 +919,12 @@ __global__ void __launch_bounds__(stoi::NT, 3) stoi_cells_kernel(StoiArgs a,
     stoi_tables(L);
     double* env = a.scratch + c * a.Mmax * 16;
     const int lag = a.lag ? a.lag[c] : 0;
-    stoi_phase_a<false>(L, a.y + a.y_offset[c], a.len, lag, a.clip != 0, nullptr, coef,
-                        a.btab + (int64_t)sig * a.NBLK * BT, a.meta[META * sig + 4], env, ts);
+    if constexpr (PRE)
+        stoi_phase_a<true>(L, nullptr, 0, 0, false, y10 + c * n10, nullptr,
+                           a.btab + (int64_t)sig * a.NBLK * BT, a.meta[META * sig + 4], env, ts);
+    else
+        stoi_phase_a<false>(L, a.y + a.y_offset[c], a.len, lag, a.clip != 0, nullptr, coef,
+                            a.btab + (int64_t)sig * a.NBLK * BT, a.meta[META * sig + 4], env, ts);
     __syncthreads();  // env rows of this workgroup are visible to it
     ts.mark(4);
     // ---- phase B: segment j, band b
@@ -873,27 +1008,63 @@ __global__ void __launch_bounds__(stoi::NT, 3) stoi_cells_kernel(StoiArgs a,
 #endif
 }
 
+// coef is a separate const __restrict__ argument so the compiler can prove it
+// is never written and read it through the scalar cache (s_load): inside the
+// argument struct it became per-lane vector loads waited on right after issue
+__global__ void __launch_bounds__(stoi::NT, 3) stoi_cells_kernel(StoiArgs a,
+                                                              const double* __restrict__ coef) {
+    __shared__ StoiLds L;
+    stoi_cells_body<false>(L, a, coef, nullptr, 0);
+}
+
+// input rates other than 16 kHz: the cells' test signals already at 10 kHz
+__global__ void __launch_bounds__(stoi::NT, 3) stoi_cells_pre_kernel(StoiArgs a,
+                                                                  const double* __restrict__ y10,
+                                                                  int64_t n10) {
+    __shared__ StoiLds L;
+    stoi_cells_body<true>(L, a, nullptr, y10, n10);
+}
+
 }  // namespace cse
 
 using namespace cse;
 
+// input rates: 16 kHz (the sweep's, resampled inside the cell kernel) and,
+// through the generic resampler, any rate in [1 kHz, 768 kHz] whose filter
+// stays below 2^25 taps
+static bool stoi_rate_ok(int sr, int64_t len) {
+    if (sr == 16000) return true;
+    if (sr < 1000 || sr > 768000) return false;
+    return 2 * resamp_for(sr, len).half + 1 < (1 << 25);
+}
+
+extern "C" int64_t cse_stoi_workspace_bytes_sr(int64_t n_sig, int64_t len, int sr) {
+    if (n_sig < 1 || len < 1 || !stoi_rate_ok(sr, len)) return -1;
+    return stoi_layout(n_sig, len, sr).total;
+}
+
 extern "C" int64_t cse_stoi_workspace_bytes(int64_t n_sig, int64_t len) {
-    if (n_sig < 1 || len < 1) return -1;
-    return stoi_layout(n_sig, len).total;
+    return cse_stoi_workspace_bytes_sr(n_sig, len, 16000);
+}
+
+extern "C" int64_t cse_stoi_scratch_bytes_sr(int64_t n_cells, int64_t len, int sr) {
+    if (n_cells < 0 || len < 1 || !stoi_rate_ok(sr, len)) return -1;
+    const StoiLayout L = stoi_layout(1, len, sr);
+    // per cell: band envelopes [Mmax][16], and at other rates the 10-kHz test signal
+    return n_cells * (L.Mmax * 16 + (sr == 16000 ? 0 : L.n10)) * 8;
 }
 
 extern "C" int64_t cse_stoi_scratch_bytes(int64_t n_cells, int64_t len) {
-    if (n_cells < 0 || len < 1) return -1;
-    return n_cells * stoi_layout(1, len).Mmax * 16 * 8;
+    return cse_stoi_scratch_bytes_sr(n_cells, len, 16000);
 }
 
 extern "C" int cse_stoi_prepare(const double* clean, int64_t n_sig, int64_t len, int sr,
                                 void* workspace, cse_stream_t stream) {
     CSE_CHECK_ARG(clean && workspace, "cse_stoi_prepare: NULL clean/workspace");
-    CSE_CHECK_ARG(sr == 16000, "cse_stoi_prepare: sr=%d (the device STOI resamples 16 kHz only)", sr);
     CSE_CHECK_ARG(n_sig >= 1 && n_sig < 65536 && len >= 1, "cse_stoi_prepare: n_sig=%lld len=%lld",
                   (long long)n_sig, (long long)len);
-    const StoiLayout L = stoi_layout(n_sig, len);
+    CSE_CHECK_ARG(stoi_rate_ok(sr, len), "cse_stoi_prepare: sr=%d not supported", sr);
+    const StoiLayout L = stoi_layout(n_sig, len, sr);
     unsigned char* ws = (unsigned char*)workspace;
     hipStream_t st = (hipStream_t)stream;
     double* coef64 = (double*)(ws + L.coef64);
@@ -904,10 +1075,21 @@ extern "C" int cse_stoi_prepare(const double* clean, int64_t n_sig, int64_t len,
     int* btab = (int*)(ws + L.btab);
     double* xtob = (double*)(ws + L.xtob);
     double4* xstat = (double4*)(ws + L.xstat);
-    hipLaunchKernelGGL(stoi_coef_kernel, dim3(1), dim3(1024), 0, st, coef64);
-    const int64_t groups = (L.n10 + 4) / 5;
-    hipLaunchKernelGGL(stoi_resample_clean_kernel, dim3(ceil_div(groups, 256), (unsigned)n_sig),
-                       dim3(256), 0, st, clean, len, L.n10, (const double*)coef64, x10);
+    if (sr == 16000) {
+        hipLaunchKernelGGL(stoi_coef_kernel, dim3(1), dim3(1024), 0, st, coef64);
+        const int64_t groups = (L.n10 + 4) / 5;
+        hipLaunchKernelGGL(stoi_resample_clean_kernel, dim3(ceil_div(groups, 256), (unsigned)n_sig),
+                           dim3(256), 0, st, clean, len, L.n10, (const double*)coef64, x10);
+    } else {
+        const Resamp r = resamp_for(sr, len);
+        double* h = (double*)(ws + L.hgen);
+        hipLaunchKernelGGL(stoi_coef_generic_kernel, dim3(1), dim3(1024), 0, st, h, r.half, r.up,
+                           r.down);
+        hipLaunchKernelGGL(stoi_resample_kernel<false>, dim3(ceil_div(L.n10, 256), (unsigned)n_sig),
+                           dim3(256), 0, st, clean, nullptr, nullptr, nullptr, 0, len,
+                           (const double*)h, 2 * r.half + 1, r.up, r.down, r.pre_pad, r.pre_rm,
+                           L.n10, x10);
+    }
     if (L.F > 0)
         hipLaunchKernelGGL(stoi_energy_kernel, dim3(ceil_div(L.F, 4), (unsigned)n_sig), dim3(256), 0,
                            st, x10, L.n10, L.F, en);
@@ -932,17 +1114,19 @@ extern "C" int cse_stoi_stamp_buffer(void* buf) {
 }
 #endif
 
-extern "C" int cse_stoi_cells(const float* y, const int64_t* y_offset, const int32_t* lag,
-                              const int32_t* sig_of, int64_t n_cells, int64_t n_sig, int64_t len,
-                              int clip, const void* workspace, void* scratch, double* stoi_out,
-                              cse_stream_t stream) {
-    CSE_CHECK_ARG(y && y_offset && sig_of && workspace && stoi_out,
-                  "cse_stoi_cells: NULL argument");
-    CSE_CHECK_ARG(n_sig >= 1 && len >= 1, "cse_stoi_cells: n_sig=%lld len=%lld", (long long)n_sig,
+static int stoi_cells_launch(const char* name, const float* y, const int64_t* y_offset,
+                             const int32_t* lag, const int32_t* sig_of, int64_t n_cells,
+                             int64_t n_sig, int64_t len, int sr, int clip, const void* workspace,
+                             void* scratch, double* stoi_out, cse_stream_t stream) {
+    CSE_CHECK_ARG(y && y_offset && sig_of && workspace && stoi_out, "%s: NULL argument", name);
+    CSE_CHECK_ARG(n_sig >= 1 && len >= 1, "%s: n_sig=%lld len=%lld", name, (long long)n_sig,
                   (long long)len);
+    CSE_CHECK_ARG(stoi_rate_ok(sr, len), "%s: sr=%d not supported", name, sr);
     if (n_cells == 0) return CSE_OK;
-    const StoiLayout L = stoi_layout(n_sig, len);
-    CSE_CHECK_ARG(L.Mmax == 0 || scratch, "cse_stoi_cells: NULL scratch");
+    const StoiLayout L = stoi_layout(n_sig, len, sr);
+    CSE_CHECK_ARG((L.Mmax == 0 && sr == 16000) || scratch, "%s: NULL scratch", name);
+    CSE_CHECK_ARG(sr == 16000 || n_cells < 65536,
+                  "%s: n_cells=%lld (< 65536 per call at sr != 16000)", name, (long long)n_cells);
     const unsigned char* ws = (const unsigned char*)workspace;
     StoiArgs a;
     a.y = y;
@@ -961,8 +1145,37 @@ extern "C" int cse_stoi_cells(const float* y, const int64_t* y_offset, const int
     a.xstat = (const double4*)(ws + L.xstat);
     a.scratch = (double*)scratch;
     a.out = stoi_out;
-    hipLaunchKernelGGL(stoi_cells_kernel, dim3((unsigned)n_cells), dim3(stoi::NT), 0,
-                       (hipStream_t)stream, a, a.coef);
-    CSE_CHECK_LAUNCH("cse_stoi_cells");
+    hipStream_t st = (hipStream_t)stream;
+    if (sr == 16000) {
+        hipLaunchKernelGGL(stoi_cells_kernel, dim3((unsigned)n_cells), dim3(stoi::NT), 0, st, a,
+                           a.coef);
+    } else {
+        // the cells' shifted, clipped outputs resampled to 10 kHz after their envelopes
+        const Resamp r = resamp_for(sr, len);
+        double* y10 = (double*)scratch + n_cells * L.Mmax * 16;
+        hipLaunchKernelGGL(stoi_resample_kernel<true>,
+                           dim3(ceil_div(L.n10, 256), (unsigned)n_cells), dim3(256), 0, st, nullptr, y, y_offset, lag, clip, len,
+                           (const double*)(ws + L.hgen), 2 * r.half + 1, r.up, r.down, r.pre_pad,
+                           r.pre_rm, L.n10, y10);
+        hipLaunchKernelGGL(stoi_cells_pre_kernel, dim3((unsigned)n_cells), dim3(stoi::NT), 0, st, a,
+                           (const double*)y10, L.n10);
+    }
+    CSE_CHECK_LAUNCH(name);
     return CSE_OK;
+}
+
+extern "C" int cse_stoi_cells(const float* y, const int64_t* y_offset, const int32_t* lag,
+                              const int32_t* sig_of, int64_t n_cells, int64_t n_sig, int64_t len,
+                              int clip, const void* workspace, void* scratch, double* stoi_out,
+                              cse_stream_t stream) {
+    return stoi_cells_launch("cse_stoi_cells", y, y_offset, lag, sig_of, n_cells, n_sig, len,
+                             16000, clip, workspace, scratch, stoi_out, stream);
+}
+
+extern "C" int cse_stoi_cells_sr(const float* y, const int64_t* y_offset, const int32_t* lag,
+                                 const int32_t* sig_of, int64_t n_cells, int64_t n_sig,
+                                 int64_t len, int sr, int clip, const void* workspace,
+                                 void* scratch, double* stoi_out, cse_stream_t stream) {
+    return stoi_cells_launch("cse_stoi_cells_sr", y, y_offset, lag, sig_of, n_cells, n_sig, len,
+                             sr, clip, workspace, scratch, stoi_out, stream);
 }

@@ -14,9 +14,10 @@ StoiPlan is the batched form the sweep uses: the clean side (10-kHz clean,
 silent-frame mask, band envelopes, segment statistics) is prepared once per
 batch of equal-length signals, then any number of cell outputs are scored
 against it, each shifted by its alignment lag and clipped like
-finalize_enhanced (speech_enhancement_comparison.py:92-106).  The device STOI
-supports the reference's working rate, 16 kHz (:381); there is no CPU
-fallback.
+finalize_enhanced (speech_enhancement_comparison.py:92-106).  The sweep runs
+at the reference's working rate, 16 kHz (:381), resampled to 10 kHz inside the
+cell kernel; other rates (1-768 kHz, 10 kHz unresampled) go through a generic
+fp64 resampler first (cse_stoi_cells_sr).  There is no CPU fallback.
 """
 
 import math
@@ -46,8 +47,6 @@ class StoiPlan:
     """Clean side of STOI for S equal-length signals (clean: [S, L] f64 cuda)."""
 
     def __init__(self, clean, sr=STOI_SR):
-        if sr != STOI_SR:
-            raise NotImplementedError(f"device STOI runs at {STOI_SR} Hz (got sr={sr})")
         if not _gpu_visible():
             raise _lib.CseError("no GPU visible: the HIP engine has no CPU fallback")
         self.lib = _lib.load()
@@ -56,14 +55,17 @@ class StoiPlan:
             raise ValueError("clean must be a [S, L] float64 cuda tensor")
         self.S, self.L = clean.shape
         self.clean = clean
-        nbytes = int(self.lib.cse_stoi_workspace_bytes(self.S, self.L))
+        self.sr = int(sr)
+        nbytes = int(self.lib.cse_stoi_workspace_bytes_sr(self.S, self.L, self.sr))
+        if nbytes < 0:
+            raise NotImplementedError(f"STOI: sample rate {sr} not supported (1000-768000 Hz)")
         self.ws = torch.empty(nbytes, dtype=torch.uint8, device=clean.device)
         _lib.check(self.lib.cse_stoi_prepare(_ptr(clean), self.S, self.L, sr, _ptr(self.ws),
                                              _stream()), "cse_stoi_prepare")
         self._scratch = None
 
     def _scratch_for(self, n):
-        nbytes = max(int(self.lib.cse_stoi_scratch_bytes(n, self.L)), 1)
+        nbytes = max(int(self.lib.cse_stoi_scratch_bytes_sr(n, self.L, self.sr)), 1)
         if self._scratch is None or self._scratch.numel() < nbytes:
             self._scratch = torch.empty(nbytes, dtype=torch.uint8, device=self.clean.device)
         return self._scratch
@@ -128,10 +130,13 @@ class StoiPlan:
         for s in range(0, n, STOI_CHUNK):
             m = min(STOI_CHUNK, n - s)
             scratch = self._scratch_for(m)
-            _lib.check(self.lib.cse_stoi_cells(
-                _ptr(y), _ptr(off[s:]), None if lg is None else _ptr(lg[s:]), _ptr(sig[s:]),
-                m, self.S, self.L, 1 if clip else 0, _ptr(self.ws), _ptr(scratch),
-                _ptr(out[s:]), _stream()), "cse_stoi_cells")
+            args = (_ptr(y), _ptr(off[s:]), None if lg is None else _ptr(lg[s:]), _ptr(sig[s:]),
+                    m, self.S, self.L)
+            tail = (1 if clip else 0, _ptr(self.ws), _ptr(scratch), _ptr(out[s:]), _stream())
+            if self.sr == STOI_SR:
+                _lib.check(self.lib.cse_stoi_cells(*args, *tail), "cse_stoi_cells")
+            else:
+                _lib.check(self.lib.cse_stoi_cells_sr(*args, self.sr, *tail), "cse_stoi_cells_sr")
         return out
 
     def score(self, y, y_offset, sig_of, lag=None, clip=True):
@@ -158,8 +163,6 @@ def stoi(x, y, fs_sig):
 def calculate_stoi(clean_reference, test_audio, sr):
     """evaluation_metrics.calculate_stoi (:30-36): trim to the common length,
     None on failure."""
-    if sr != STOI_SR:
-        raise NotImplementedError(f"device STOI runs at {STOI_SR} Hz (got sr={sr})")
     try:
         n = min(len(clean_reference), len(test_audio))
         return stoi(np.asarray(clean_reference)[:n], np.asarray(test_audio)[:n], sr)

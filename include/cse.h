@@ -340,8 +340,13 @@ int cse_xcorr_lag(const float* head, const int64_t* head_offset, const int32_t* 
  * STOI (pystoi 0.4.1 `stoi(clean, enhanced, sr, extended=False)`, the score of
  * evaluation_metrics.py:30-36 that the reference's sweep optimises at
  * speech_enhancement_comparison.py:180, and its noisy baseline at :115).
- * Only sr = 16000 (the reference's target rate, :381) is supported: both
- * signals are resampled to 10 kHz with Octave's resample filter.
+ * Both signals are resampled to 10 kHz with Octave's resample filter
+ * (pystoi utils.resample_oct).  sr = 16000, the reference's working rate
+ * (:381) and the sweep's, is resampled inside the cell kernel; any other
+ * rate in [1000, 768000] (filter below 2^25 taps; 10000 = no resampling)
+ * goes through a generic fp64 polyphase resampler first (r06).  Workspace
+ * and scratch sizes then depend on the rate: the _sr size functions (the
+ * plain ones are their sr = 16000 case).
  *
  * cse_stoi_prepare: the clean side, once per signal batch — clean [n_sig][len]
  *   f64 -> workspace of cse_stoi_workspace_bytes(n_sig, len) bytes (10-kHz clean
@@ -359,11 +364,19 @@ int cse_xcorr_lag(const float* head, const int64_t* head_offset, const int32_t* 
  */
 int64_t cse_stoi_workspace_bytes(int64_t n_sig, int64_t len);
 int64_t cse_stoi_scratch_bytes(int64_t n_cells, int64_t len);
+int64_t cse_stoi_workspace_bytes_sr(int64_t n_sig, int64_t len, int sr);  /* -1: rate unsupported */
+int64_t cse_stoi_scratch_bytes_sr(int64_t n_cells, int64_t len, int sr);
 int cse_stoi_prepare(const double* clean, int64_t n_sig, int64_t len, int sr, void* workspace,
                      cse_stream_t stream);
+/* cse_stoi_cells scores signals at 16 kHz; cse_stoi_cells_sr at the rate the
+ * workspace was prepared for (n_cells < 65536 per call at other rates). */
 int cse_stoi_cells(const float* y, const int64_t* y_offset, const int32_t* lag,
                    const int32_t* sig_of, int64_t n_cells, int64_t n_sig, int64_t len, int clip,
                    const void* workspace, void* scratch, double* stoi, cse_stream_t stream);
+int cse_stoi_cells_sr(const float* y, const int64_t* y_offset, const int32_t* lag,
+                      const int32_t* sig_of, int64_t n_cells, int64_t n_sig, int64_t len, int sr,
+                      int clip, const void* workspace, void* scratch, double* stoi,
+                      cse_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -68,6 +68,29 @@ def test_version_and_error_channel(lib):
         assert lib.cse_enhance_cells_short_hop(n_fft, n, *args) == 0, lib.cse_last_error()
 
 
+def test_stoi_rates(lib):
+    """STOI sizes per input rate: 16 kHz is the plain functions' case, other
+    rates in [1 kHz, 768 kHz] add the generic filter (2L + 1 taps) and the
+    cells' 10-kHz test signals; unsupported rates report -1 and are refused."""
+    n = 48000
+    assert lib.cse_stoi_workspace_bytes_sr(2, n, 16000) == lib.cse_stoi_workspace_bytes(2, n)
+    assert lib.cse_stoi_scratch_bytes_sr(3, n, 16000) == lib.cse_stoi_scratch_bytes(3, n)
+    for sr in (999, 768001, -16000):
+        assert lib.cse_stoi_workspace_bytes_sr(1, n, sr) == -1
+        assert lib.cse_stoi_scratch_bytes_sr(1, n, sr) == -1
+    for sr in (8000, 10000, 22050, 44100, 48000):
+        assert lib.cse_stoi_workspace_bytes_sr(1, n, sr) > 0
+        # scratch: envelopes + the 10-kHz signal, ceil(n 10000 / sr) doubles per cell
+        n10 = -(-n * 10000 // sr)
+        assert lib.cse_stoi_scratch_bytes_sr(1, n, sr) >= 8 * n10
+    rc = lib.cse_stoi_prepare(ctypes.c_void_p(16), 1, n, 500, ctypes.c_void_p(16), None)
+    assert rc == -1 and b"sr=500" in lib.cse_last_error()
+    rc = lib.cse_stoi_cells_sr(ctypes.c_void_p(16), ctypes.c_void_p(16), None, ctypes.c_void_p(16),
+                               0, 1, n, 900000, 1, ctypes.c_void_p(16), None, ctypes.c_void_p(16),
+                               None)
+    assert rc == -1 and b"sr=900000" in lib.cse_last_error()
+
+
 def test_short_hop_groups_pack_last():
     """pack_waves puts the short-hop groups after the sweep-hop ones (their
     own launch: GridPlan.launch), whatever their cost; main_slots counts the
