@@ -51,6 +51,7 @@ EXPORTS = ("cse_version", "cse_last_error", "cse_cells_per_group", "cse_stft",
            "cse_noise_estimate", "cse_noise_smooth", "cse_noise_median",
            "cse_noise_percentile_med", "cse_noise_percentile_med2", "cse_noise_percentile_quad", "cse_noise_min_tracking_med", "cse_noise_finish",
            "cse_noise_invert", "cse_istft_norm", "cse_enhance_cells", "cse_enhance_cells_short_hop",
+           "cse_enhance_cells_generic",
            "cse_xcorr_workspace_bytes", "cse_xcorr_prepare", "cse_xcorr_lag",
            "cse_stoi_workspace_bytes", "cse_stoi_scratch_bytes", "cse_stoi_prepare",
            "cse_stoi_cells", "cse_stoi_workspace_bytes_sr", "cse_stoi_scratch_bytes_sr",
@@ -142,6 +143,8 @@ def load(path=LIB_PATH):
     lib.cse_enhance_cells.argtypes = [i32, i64, P, i64, P, P, P, P, i64, P, P, P, P]
     lib.cse_enhance_cells_short_hop.restype = i32
     lib.cse_enhance_cells_short_hop.argtypes = [i32, i64, P, i64, P, P, P, P, i64, P, P, P]
+    lib.cse_enhance_cells_generic.restype = i32
+    lib.cse_enhance_cells_generic.argtypes = [i32, i64, P, i64, P, P, P, P, i64, P, P, P, P]
     # the kernels read the cell/job tables laid out as this package packs them:
     # refuse a library of another ABI revision.  The packer (engine.pack_waves)
     # takes the slot-group size from the library itself; it must be usable.

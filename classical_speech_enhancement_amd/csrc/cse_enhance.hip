@@ -1559,6 +1559,9 @@ __global__ void __launch_bounds__(WG<NFFT>::THREADS, CSE_WAVES_PER_SIMD)
     enhance_group<NFFT, false, NFFT == 512 ? 32 : 64, 64>(a);
 }
 
+// cse_enhance_generic.hip includes this file for the gain functions above
+// (CSE_ENHANCE_DEVICE_ONLY): no kernel instantiations, no entry points.
+#ifndef CSE_ENHANCE_DEVICE_ONLY
 // The two n_fft halves can be compiled as separate translation units (with
 // their own code-generation flags): cse_enhance_512.hip defines
 // CSE_ENHANCE_ONLY=512 and holds the 512 kernels, cse_enhance_1024.hip the
@@ -1589,8 +1592,11 @@ const void* enhance_fn_1024(bool out) {
 const void* enhance_fn_512(bool out);  // cse_enhance_512.hip
 #endif
 #endif  // !CSE_ENHANCE_SHORT
+#endif  // !CSE_ENHANCE_DEVICE_ONLY
 
 }  // namespace cse
+
+#ifndef CSE_ENHANCE_DEVICE_ONLY
 
 #if defined(CSE_ENH_STAMPS) && !defined(CSE_ENHANCE_SHORT)
 // analysis builds only: per-workgroup stage cycles into buf [n_groups][10]
@@ -1690,3 +1696,4 @@ extern "C" int cse_enhance_cells_short_hop(int n_fft, int64_t len, const cse_cel
                           noise, clean, y_out, out_len, nullptr, sse, finite, stream);
 }
 #endif  // the C entry points
+#endif  // !CSE_ENHANCE_DEVICE_ONLY

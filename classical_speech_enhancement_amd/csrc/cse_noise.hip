@@ -704,7 +704,7 @@ __device__ __forceinline__ float rcp_rn(float x) {
 // flattened one-thread-per-bin form) ran the rows' stores at 2.5 TB/s; the
 // tiled block stores at 4.7 TB/s (tools/micro/row_store.hip).
 constexpr int FIN_F = 16;     // frames per tile
-constexpr int FIN_MAXU = 4;   // bins per thread (B <= 1,024)
+constexpr int FIN_MAXU = 5;   // bins per thread (B <= 1,280: n_fft up to 2048, r06)
 __global__ void __launch_bounds__(256) finish_kernel(const cse_noise_job_t* __restrict__ jobs,
                                                      int B, const float* __restrict__ src,
                                                      float* __restrict__ dst) {
@@ -1115,6 +1115,12 @@ extern "C" int cse_noise_finish(const cse_noise_job_t* jobs, int n_jobs, int64_t
     CSE_CHECK_ARG(B <= 256 * FIN_MAXU, "cse_noise_finish: B=%d > %d", B, 256 * FIN_MAXU);
     const dim3 grid((unsigned)n_sig, (unsigned)n_jobs);
     const size_t lds = (size_t)FIN_F * B * 4;
+    if (lds > 65536 && hipFuncSetAttribute((const void*)finish_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds) != hipSuccess) {
+        ::cse::set_error("cse_noise_finish: cannot reserve %zu bytes of LDS", lds);
+        return CSE_ELAUNCH;
+    }
     hipLaunchKernelGGL(finish_kernel, grid, dim3(256), lds, (hipStream_t)stream, jobs, B, src, dst);
     CSE_CHECK_LAUNCH("cse_noise_finish");
     return CSE_OK;

@@ -27,16 +27,18 @@ __device__ __forceinline__ int64_t reflect_index(int64_t p, int64_t len) {
 // sincospi / cospi per point), and only frames that reach past either end of
 // the signal take the 64-bit reflect arithmetic.  Every element sees the same
 // operations as before, so Y and P are bit-identical to the one-frame form.
+// (n_fft 2048, r06: one frame per workgroup, the 64-KB static LDS limit)
 constexpr int STFT_FPB = 4;
+__host__ __device__ constexpr int stft_fpb(int nfft) { return nfft > 1024 ? 1 : STFT_FPB; }
 template <int NFFT>
 __global__ void __launch_bounds__(256) stft_kernel(const double* __restrict__ x,
                                                    const double* __restrict__ x_sub,
                                                    int64_t len, int hop, int T,
                                                    float2* __restrict__ Y,
                                                    double* __restrict__ P) {
-    constexpr int LOG2N = (NFFT == 512) ? 9 : 10;
+    constexpr int LOG2N = __builtin_ctz(NFFT);
     constexpr int B = NFFT / 2 + 1;
-    constexpr int F = STFT_FPB;
+    constexpr int F = stft_fpb(NFFT);
     __shared__ double re[F][NFFT], im[F][NFFT];
     __shared__ double twr[NFFT / 2], twi[NFFT / 2], win[NFFT];
     const int tb = blockIdx.x * F;
@@ -282,24 +284,46 @@ extern "C" int cse_stft(const double* x, const double* x_sub, int64_t n_sig, int
     CSE_CHECK_ARG(x != nullptr, "cse_stft: x is NULL");
     CSE_CHECK_ARG(n_sig > 0 && n_sig < 65536, "cse_stft: n_sig=%lld out of range", (long long)n_sig);
     CSE_CHECK_ARG(len >= 1, "cse_stft: len=%lld", (long long)len);
-    CSE_CHECK_ARG(n_fft == 512 || n_fft == 1024, "cse_stft: n_fft=%d (512|1024)", n_fft);
+    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 2048 && (n_fft & (n_fft - 1)) == 0,
+                  "cse_stft: n_fft=%d (a power of two in [64, 2048])", n_fft);
     CSE_CHECK_ARG(hop >= 1 && hop <= n_fft, "cse_stft: hop=%d", hop);
     const int T = n_frames_for(len, hop);
-    dim3 grid((unsigned)ceil_div(T, STFT_FPB), (unsigned)n_sig);
-    if (n_fft == 512)
-        hipLaunchKernelGGL(stft512_kernel, dim3((unsigned)ceil_div(T, S512_FPB), (unsigned)n_sig),
-                           dim3(256), 0, (hipStream_t)stream, x, x_sub, len, hop, T, (float2*)Y,
-                           P);
-    else
-        hipLaunchKernelGGL(stft_kernel<1024>, grid, dim3(256), 0, (hipStream_t)stream, x, x_sub,
-                           len, hop, T, (float2*)Y, P);
+    dim3 grid((unsigned)ceil_div(T, stft_fpb(n_fft)), (unsigned)n_sig);
+    hipStream_t st = (hipStream_t)stream;
+    switch (n_fft) {  // 512: its own register-resident form; the rest radix 2 in LDS
+        case 512:
+            hipLaunchKernelGGL(stft512_kernel, dim3((unsigned)ceil_div(T, S512_FPB), (unsigned)n_sig),
+                               dim3(256), 0, st, x, x_sub, len, hop, T, (float2*)Y, P);
+            break;
+        case 1024:
+            hipLaunchKernelGGL(stft_kernel<1024>, grid, dim3(256), 0, st, x, x_sub, len, hop, T,
+                               (float2*)Y, P);
+            break;
+        case 64:
+            hipLaunchKernelGGL(stft_kernel<64>, grid, dim3(256), 0, st, x, x_sub, len, hop, T,
+                               (float2*)Y, P);
+            break;
+        case 128:
+            hipLaunchKernelGGL(stft_kernel<128>, grid, dim3(256), 0, st, x, x_sub, len, hop, T,
+                               (float2*)Y, P);
+            break;
+        case 256:
+            hipLaunchKernelGGL(stft_kernel<256>, grid, dim3(256), 0, st, x, x_sub, len, hop, T,
+                               (float2*)Y, P);
+            break;
+        default:  // 2048
+            hipLaunchKernelGGL(stft_kernel<2048>, grid, dim3(256), 0, st, x, x_sub, len, hop, T,
+                               (float2*)Y, P);
+            break;
+    }
     CSE_CHECK_LAUNCH("cse_stft");
     return CSE_OK;
 }
 
 extern "C" int cse_istft_norm(int n_fft, int hop, int64_t len, float* out, cse_stream_t stream) {
     CSE_CHECK_ARG(out != nullptr, "cse_istft_norm: out is NULL");
-    CSE_CHECK_ARG(n_fft == 512 || n_fft == 1024, "cse_istft_norm: n_fft=%d", n_fft);
+    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 2048 && (n_fft & (n_fft - 1)) == 0,
+                  "cse_istft_norm: n_fft=%d", n_fft);
     CSE_CHECK_ARG(hop >= 1 && hop <= n_fft && len >= 1, "cse_istft_norm: hop=%d len=%lld", hop,
                   (long long)len);
     const int T = n_frames_for(len, hop);

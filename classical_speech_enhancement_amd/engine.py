@@ -60,9 +60,24 @@ def _at(t, k):
 
 
 # hops of the sweep kernels (cse_enhance_cells) and the short hops of
-# cse_enhance_cells_short_hop, per n_fft
+# cse_enhance_cells_short_hop, per n_fft; every other power-of-two n_fft in
+# [64, 2048] and hop in [1, n_fft] goes to cse_enhance_cells_generic
 HOPS = (128, 256)
 SHORT_HOPS = {512: (32, 64), 1024: (64,)}
+MAIN, SHORT, GENERIC = 0, 1, 2
+
+
+def route(n_fft, hop):
+    """Which enhance kernel runs (n_fft, hop): MAIN, SHORT, GENERIC, or None
+    (not supported)."""
+    n_fft, hop = int(n_fft), int(hop)
+    if n_fft in (512, 1024) and hop in HOPS:
+        return MAIN
+    if hop in SHORT_HOPS.get(n_fft, ()):
+        return SHORT
+    if 64 <= n_fft <= 2048 and n_fft & (n_fft - 1) == 0 and 1 <= hop <= n_fft:
+        return GENERIC
+    return None
 
 
 def _stream():
@@ -393,7 +408,7 @@ class GridPlan:
         self.cells = cells
         packed, self.order = pack_waves(cells, n_fft)
         self.n_packed = len(packed)
-        self.n_main = main_slots(packed)
+        self.split = route_slots(packed, n_fft)
         self.cells_d = torch.from_numpy(packed.view(np.uint8).copy()).to(dev)
         self.g_out = torch.zeros(max(g_total, 1), dtype=torch.float32, device=dev) if want_g else None
         self.y_all = y_all
@@ -417,7 +432,7 @@ class GridPlan:
                 head_off = np.arange(len(items), dtype=np.int64) * self.xc_n
                 self.cells["out_offset"] = head_off
                 packed, _ = pack_waves(self.cells, n_fft)
-                assert main_slots(packed) == self.n_main
+                assert route_slots(packed, n_fft) == self.split
                 self.cells_d = torch.from_numpy(packed.view(np.uint8).copy()).to(dev)
             self.head_off = torch.as_tensor(head_off, device=dev)
             self.sig_of = torch.as_tensor(sig.astype(np.int32), device=dev)
@@ -533,21 +548,30 @@ class GridPlan:
             yo, olen = self.head, self.xc_n
         else:
             yo, olen = None, 0
-        self.launch(self.cells_d, self.n_packed, self.n_main, yo, olen, self.g_out, self.sse_d,
-                    self.fin_d, _stream(), "cse_enhance_cells")
+        self.launch(self.cells_d, self.split, yo, olen, self.g_out, self.sse_d, self.fin_d,
+                    _stream(), "cse_enhance_cells")
 
-    def launch(self, cells_d, n, n_main, yo, olen, g, sse, fin, st, what):
-        """The enhance launches over packed cells: slots [0, n_main) at the
-        sweep hops (cse_enhance_cells, one kernel), the rest at the short hops
-        (cse_enhance_cells_short_hop; pack_waves puts those groups last)."""
+    def launch(self, cells_d, split, yo, olen, g, sse, fin, st, what):
+        """The enhance launches over packed cells, split = (main, short,
+        generic) slot counts in that order (pack_waves): the sweep hops
+        (cse_enhance_cells, one kernel), the short hops
+        (cse_enhance_cells_short_hop), every other shape
+        (cse_enhance_cells_generic)."""
         args = (_ptr(self.Ybuf), _ptr(self.pool), _ptr(self.clean), _ptr(yo), olen)
+        n_main, n_short, n_gen = split
+        k = _lib.CELL_DTYPE.itemsize
         if n_main:
             _lib.check(self.lib.cse_enhance_cells(self.n_fft, self.L, _ptr(cells_d), n_main, *args,
                                                   _ptr(g), _ptr(sse), _ptr(fin), st), what)
-        if n > n_main:
+        if n_short:
             _lib.check(self.lib.cse_enhance_cells_short_hop(
-                self.n_fft, self.L, _at(cells_d, n_main * _lib.CELL_DTYPE.itemsize), n - n_main,
-                *args, _at(sse, n_main), _at(fin, n_main), st), what + "(short hop)")
+                self.n_fft, self.L, _at(cells_d, n_main * k), n_short, *args, _at(sse, n_main),
+                _at(fin, n_main), st), what + "(short hop)")
+        if n_gen:
+            o = n_main + n_short
+            _lib.check(self.lib.cse_enhance_cells_generic(
+                self.n_fft, self.L, _at(cells_d, o * k), n_gen, *args, _ptr(g), _at(sse, o),
+                _at(fin, o), st), what + "(generic)")
 
     def execute(self, noisy, clean=None):
         self.prepare(noisy, clean)
@@ -581,7 +605,7 @@ class GridPlan:
         cd = torch.from_numpy(packed.view(np.uint8).copy()).to(self.device)
         sse = torch.zeros(len(packed), dtype=torch.float64, device=self.device)
         fin = torch.zeros(len(packed), dtype=torch.uint8, device=self.device)
-        self.launch(cd, len(packed), main_slots(packed), None, 0, None, sse, fin, st,
+        self.launch(cd, route_slots(packed, self.n_fft), None, 0, None, sse, fin, st,
                     "cse_enhance_cells(aligned)")
         self.rerun = (sel, order, sse, fin)
 
@@ -631,11 +655,12 @@ class MultiPlan:
                 raise ValueError(f"signal index {sig} out of range")
             ck = (alg, hop, nf, p["noise_method"])
             if ck not in checked:  # per distinct (algorithm, hop, n_fft, method)
-                if nf not in (512, 1024) or hop not in HOPS + SHORT_HOPS[nf]:
-                    raise ValueError("engine supports n_fft 512 at hop 32, 64, 128, 256 and "
-                                     "n_fft 1024 at hop 64, 128, 256")
-                if want_g and hop not in HOPS:
-                    raise ValueError(f"gain matrices only at hop in {HOPS}")
+                r = route(nf, hop)
+                if r is None:
+                    raise ValueError(f"engine supports n_fft a power of two in [64, 2048] and "
+                                     f"hop in [1, n_fft] (got n_fft={nf}, hop={hop})")
+                if want_g and r == SHORT:
+                    raise ValueError(f"gain matrices not at the short hops (n_fft={nf}, hop={hop})")
                 noise_key(alg, p, n_frames(L, hop))  # validates the method
                 if (p["noise_method"] == "true_noise" and not with_clean
                         and n_frames(L, hop) >= 5):
@@ -727,14 +752,19 @@ def pack_waves(cells, n_fft):
     slot i, or -1 for padding.  Groups are ordered longest-first (frames x
     algorithm cost, then by key) so the launch ends on short workgroups;
     neighbours share rows, and the kernel's XCD remap keeps neighbours on one
-    XCD's L2.  Groups at the short hops (SHORT_HOPS) come after all others:
-    they go to a launch of their own (GridPlan.launch, main_slots).
+    XCD's L2.  Groups at the short hops (SHORT_HOPS) come after the sweep
+    hops' and the groups of every other shape after those: each class goes to
+    a launch of its own (GridPlan.launch, route_slots).  n_fft other than
+    512 / 1024 is all generic: one cell per slot (the generic kernel runs one
+    workgroup per cell), in the given order.
     Vectorised (numpy): a 100k-cell table packs in milliseconds.
     """
-    per = _lib.cells_per_group(n_fft)
     n = len(cells)
     if n == 0:
         return np.zeros(0, dtype=_lib.CELL_DTYPE), np.zeros(0, dtype=np.int64)
+    if int(n_fft) not in (512, 1024):
+        return cells.copy(), np.arange(n, dtype=np.int64)
+    per = _lib.cells_per_group(n_fft)
     keys = np.stack([cells[f].astype(np.int64) for f in
                      ("hop", "algo", "y_offset", "noise_offset", "noise_stride",
                       "clean_offset", "lag")], axis=1)
@@ -748,8 +778,8 @@ def pack_waves(cells, n_fft):
         if code >= 0:
             cost_of[code] = ALGO_COST[name]
     cost = (1 + 16000 // uniq[:, 0]) * cost_of[uniq[:, 1]]
-    short = ~np.isin(uniq[:, 0], HOPS)
-    gorder = np.lexsort((np.arange(G), -cost, short))   # longest first, then key order
+    cls = np.array([_cls(n_fft, h) for h in uniq[:, 0]], dtype=np.int64)
+    gorder = np.lexsort((np.arange(G), -cost, cls))     # longest first, then key order
     slot_base = np.zeros(G, dtype=np.int64)
     slot_base[gorder] = np.concatenate([[0], np.cumsum(nslots[gorder])[:-1]])
     # rank of each cell inside its group, in the cells' original order
@@ -775,9 +805,21 @@ def pack_waves(cells, n_fft):
     return packed, order
 
 
-def main_slots(packed):
-    """Packed slots of the sweep-hop groups (pack_waves puts them first)."""
-    return int(np.count_nonzero(np.isin(packed["hop"], HOPS)))
+def _cls(n_fft, hop):
+    """route() for packing: shapes no kernel supports count as generic (that
+    kernel's entry point refuses them)."""
+    r = route(n_fft, hop)
+    return GENERIC if r is None else r
+
+
+def route_slots(packed, n_fft):
+    """(sweep-hop, short-hop, generic) slot counts of a packed table, which
+    pack_waves orders that way."""
+    per = [0, 0, 0]
+    hops, counts = np.unique(packed["hop"], return_counts=True)
+    for h, k in zip(hops.tolist(), counts.tolist()):
+        per[_cls(n_fft, h)] += int(k)
+    return per[MAIN], per[SHORT], per[GENERIC]
 
 
 def snr_db(sse, clean_power):

@@ -324,12 +324,36 @@ def gen_short_hops(R):
     print("short_hops_0p5s.npz", len(out))
 
 
+GENERIC_SHAPES = ((128, 32), (256, 64), (512, 160), (512, 512), (1024, 512), (2048, 512))
+
+
+def gen_generic_shapes(R):
+    """Fixture: every algorithm x method at STFT shapes outside the sweep
+    kernels' (cse_enhance_cells_generic) on a 0.5-s pair, float32-stored."""
+    clean, noisy = make_pair(13, seconds=0.5)
+    clean = clean.astype(np.float32).astype(np.float64)
+    out = {"clean": clean.astype(np.float32), "noisy": noisy, "synth": np.asarray([13, 0.5])}
+    for alg, base in CELLS.items():
+        for method in ("percentile", "min_tracking", "true_noise"):
+            for n_fft, hop in GENERIC_SHAPES:
+                kw = dict(base, n_fft=n_fft, hop_length=hop, noise_percentile=10.0,
+                          noise_method=method)
+                if method == "true_noise":
+                    kw["clean_audio"] = clean
+                y = R[alg](noisy, 16000, **kw)
+                out[f"y|{alg}|{method}|{n_fft}|{hop}"] = np.asarray(y, dtype=np.float32)
+    np.savez_compressed(os.path.join(OUT, "generic_shapes_0p5s.npz"), **out)
+    print("generic_shapes_0p5s.npz", len(out))
+
+
 if __name__ == "__main__":
     R = ref_modules()
     which = sys.argv[1:] or ["algorithms", "config1", "short", "presentation", "grid", "tiny",
-                             "noise_params", "short_hops"]
+                             "noise_params", "short_hops", "generic_shapes"]
     if "short_hops" in which:
         gen_short_hops(R)
+    if "generic_shapes" in which:
+        gen_generic_shapes(R)
     if "algorithms" in which:
         gen_algorithms(R)
     if "config1" in which:

@@ -40,6 +40,13 @@ def test_version_and_error_channel(lib):
     assert b"x is NULL" in lib.cse_last_error()
     rc = lib.cse_stft(ctypes.c_void_p(16), None, 1, 100, 500, 128, None, None, None)
     assert rc == -1 and b"n_fft" in lib.cse_last_error()
+    rc = lib.cse_stft(ctypes.c_void_p(16), None, 1, 100, 4096, 128, None, None, None)
+    assert rc == -1 and b"n_fft" in lib.cse_last_error()
+    args = (100, ctypes.c_void_p(16), 1, ctypes.c_void_p(16), ctypes.c_void_p(16), None, None, 0,
+            None, None, None, None)
+    for bad in (32, 384, 4096):
+        rc = lib.cse_enhance_cells_generic(bad, *args)
+        assert rc == -1 and b"cse_enhance_cells_generic: n_fft" in lib.cse_last_error()
     rc = lib.cse_enhance_cells(256, 100, ctypes.c_void_p(16), 1, ctypes.c_void_p(16),
                                ctypes.c_void_p(16), None, None, 0, None, None, None, None)
     assert rc == -1 and b"n_fft" in lib.cse_last_error()
@@ -91,24 +98,34 @@ def test_stoi_rates(lib):
     assert rc == -1 and b"sr=900000" in lib.cse_last_error()
 
 
-def test_short_hop_groups_pack_last():
-    """pack_waves puts the short-hop groups after the sweep-hop ones (their
-    own launch: GridPlan.launch), whatever their cost; main_slots counts the
-    sweep-hop slots."""
-    from classical_speech_enhancement_amd.engine import main_slots, pack_waves
-    cells = np.zeros(9, dtype=_lib.CELL_DTYPE)
-    cells["algo"] = [0, 3, 3, 1, 0, 3, 2, 2, 3]
-    cells["hop"] = [32, 256, 64, 128, 128, 32, 256, 64, 128]
-    cells["y_offset"] = np.arange(9)
+def test_route_classes_pack_in_order():
+    """pack_waves puts the short-hop groups after the sweep-hop ones and the
+    generic shapes last (each class its own launch: GridPlan.launch),
+    whatever their cost; route_slots counts the three parts."""
+    from classical_speech_enhancement_amd.engine import (GENERIC, MAIN, SHORT, pack_waves, route,
+                                                         route_slots)
+    cells = np.zeros(11, dtype=_lib.CELL_DTYPE)
+    cells["algo"] = [0, 3, 3, 1, 0, 3, 2, 2, 3, 3, 1]
+    cells["hop"] = [32, 256, 64, 128, 128, 32, 256, 64, 128, 160, 512]
+    cells["y_offset"] = np.arange(11)
     packed, order = pack_waves(cells, 512)
     G = _lib.cells_per_group(512)
-    k = main_slots(packed)
-    assert k == 5 * G  # five sweep-hop cells, each its own group (distinct rows)
-    assert set(packed["hop"][:k].tolist()) == {128, 256}
-    assert set(packed["hop"][k:].tolist()) == {32, 64}
-    assert sorted(order[order >= 0].tolist()) == list(range(9))
+    k_main, k_short, k_gen = route_slots(packed, 512)
+    assert k_main == 5 * G  # five sweep-hop cells, each its own group (distinct rows)
+    assert (k_short, k_gen) == (4 * G, 2 * G)
+    assert set(packed["hop"][:k_main].tolist()) == {128, 256}
+    assert set(packed["hop"][k_main:k_main + k_short].tolist()) == {32, 64}
+    assert set(packed["hop"][k_main + k_short:].tolist()) == {160, 512}
+    assert sorted(order[order >= 0].tolist()) == list(range(11))
     # inside each part: longest first (hop 32 OMLSA leads the short part)
-    assert packed[k]["hop"] == 32 and packed[k]["algo"] == 3
+    assert packed[k_main]["hop"] == 32 and packed[k_main]["algo"] == 3
+    # other n_fft: every cell generic, one slot each, in the given order
+    p2, o2 = pack_waves(cells, 256)
+    assert len(p2) == 11 and o2.tolist() == list(range(11))
+    assert route_slots(p2, 256) == (0, 0, 11)
+    assert route(512, 128) == MAIN and route(1024, 64) == SHORT and route(512, 160) == GENERIC
+    assert route(2048, 512) == GENERIC and route(1024, 512) == GENERIC
+    assert route(500, 100) is None and route(4096, 1024) is None and route(256, 300) is None
 
 
 def test_cells_per_group_matches_header(lib):

@@ -105,10 +105,10 @@ def test_short_hops_match_reference_golden(P):
 
 
 def test_short_and_sweep_hops_in_one_plan(P):
-    """One plan mixing sweep-hop and short-hop cells (two launches over one
-    packed table) equals the cells run one plan each (the same cell code; a
-    misplaced output pointer would show as a gross error); gain matrices at a
-    short hop and unsupported hops raise."""
+    """One plan mixing sweep-hop, short-hop and generic-shape cells (three
+    launches over one packed table) equals the cells run one plan each (the
+    same cell code; a misplaced output pointer would show as a gross error);
+    gain matrices at a short hop and unsupported shapes raise."""
     import torch
     from classical_speech_enhancement_amd.engine import Engine
     clean, noisy = make_pair(5, seconds=0.5)
@@ -119,7 +119,8 @@ def test_short_and_sweep_hops_in_one_plan(P):
     for s in (0, 1):
         for alg, kw in (("wiener", CELLS["wiener"]), ("omlsa", CELLS["omlsa"]),
                         ("ss", CELLS["ss"]), ("mmse", CELLS["mmse"])):
-            for n_fft, hop in ((512, 128), (512, 32), (1024, 64), (1024, 256), (512, 64)):
+            for n_fft, hop in ((512, 128), (512, 32), (1024, 64), (1024, 256), (512, 64),
+                               (512, 160), (1024, 512)):
                 specs.append((s, alg, dict(kw, n_fft=n_fft, hop_length=hop, noise_percentile=10.0,
                                            noise_method="min_tracking")))
     together = eng.run(x, specs, clean=c, want_waveforms=True)
@@ -133,7 +134,10 @@ def test_short_and_sweep_hops_in_one_plan(P):
     with pytest.raises(ValueError, match="gain matrices"):
         eng.run(x, specs[1:2], clean=c, want_gains=True)
     with pytest.raises(ValueError, match="engine supports"):
-        eng.run(x, [(0, "wiener", dict(CELLS["wiener"], n_fft=1024, hop_length=32,
+        eng.run(x, [(0, "wiener", dict(CELLS["wiener"], n_fft=1024, hop_length=2048,
+                                       noise_percentile=10.0, noise_method="percentile"))])
+    with pytest.raises(ValueError, match="engine supports"):
+        eng.run(x, [(0, "wiener", dict(CELLS["wiener"], n_fft=400, hop_length=160,
                                        noise_percentile=10.0, noise_method="percentile"))])
 
 
@@ -151,6 +155,80 @@ def test_short_hops_10s_vs_oracle(P, n_fft, hop):
         y = _fn(P, alg)(noisy, 16000, **kw)
         ref = ORACLE[alg](noisy, 16000, **kw)
         assert rel_l2(y, ref) <= TOL and rel_max(y, ref) <= TOL, (alg, rel_l2(y, ref))
+
+
+def test_generic_shapes_match_reference_golden(P):
+    """cse_enhance_cells_generic (any power-of-two n_fft in [64, 2048], any hop
+    up to n_fft; here 128/32, 256/64, 512/160, 512/512, 1024/512, 2048/512)
+    through the plugins against the reference's outputs (float32-stored)."""
+    g = load_golden("generic_shapes_0p5s.npz")
+    noisy, clean = g["noisy"], g["clean"].astype(np.float64)
+    n = 0
+    for key in g.files:
+        if not key.startswith("y|"):
+            continue
+        alg, method, n_fft, hop = key.split("|")[1:]
+        kw = dict(CELLS[alg], n_fft=int(n_fft), hop_length=int(hop), noise_percentile=10.0,
+                  noise_method=method)
+        if method == "true_noise":
+            kw["clean_audio"] = clean
+        y = _fn(P, alg)(noisy, 16000, **kw)
+        ref = g[key].astype(np.float64)
+        assert y.shape == ref.shape, key
+        assert rel_l2(y, ref) <= TOL and rel_max(y, ref) <= TOL, (key, rel_l2(y, ref))
+        n += 1
+    assert n == 72
+
+
+@pytest.mark.parametrize("n_fft,hop", [(256, 80), (512, 160), (2048, 512)])
+def test_generic_shapes_10s_vs_oracle(P, n_fft, hop):
+    """10-s signals at generic shapes, every algorithm, against the oracle."""
+    clean, noisy = make_pair(4, seconds=10.0)
+    for alg, method in (("ss", "true_noise"), ("wiener", "percentile"),
+                        ("mmse", "min_tracking"), ("omlsa", "min_tracking")):
+        kw = dict(CELLS[alg], n_fft=n_fft, hop_length=hop, noise_percentile=10.0,
+                  noise_method=method)
+        if method == "true_noise":
+            kw["clean_audio"] = clean
+        y = _fn(P, alg)(noisy, 16000, **kw)
+        ref = ORACLE[alg](noisy, 16000, **kw)
+        assert rel_l2(y, ref) <= TOL and rel_max(y, ref) <= TOL, (alg, rel_l2(y, ref))
+
+
+def test_generic_gains_and_sse_match_oracle():
+    """The generic kernel's gain matrices against the oracle's gain loops, and
+    its SNR error sums against the oracle's (clean-scored, lag 0)."""
+    import torch
+    from classical_speech_enhancement_amd.engine import Engine
+    from oracle import gain_ref
+    clean, noisy = make_pair(6, seconds=1.0)
+    eng = Engine()
+    x = torch.as_tensor(noisy).cuda().view(1, -1)
+    c = torch.as_tensor(clean).cuda().view(1, -1)
+    specs = [(0, "wiener", dict(CELLS["wiener"], n_fft=256, hop_length=64,
+                                 noise_percentile=20.0, noise_method="min_tracking")),
+             (0, "mmse", dict(CELLS["mmse"], n_fft=512, hop_length=160, noise_percentile=10.0,
+                               noise_method="percentile")),
+             (0, "omlsa", dict(CELLS["omlsa"], n_fft=2048, hop_length=512,
+                                noise_percentile=10.0, noise_method="min_tracking"))]
+    res = eng.run(x, specs, clean=c, want_gains=True)
+    for i, ((sig, alg, p), G) in enumerate(zip(specs, res["G"])):
+        Y, Pw, N = gain_ref.analyse(noisy, 16000, p["n_fft"], p["hop_length"],
+                                    p["noise_percentile"], p["noise_method"], None,
+                                    {"wiener": 1e-10, "mmse": 1e-12, "omlsa": 1e-10}[alg])
+        if alg == "wiener":
+            ref = gain_ref.wiener_gains(Pw, np.maximum(N, 1e-10), p["alpha"], p["gain_floor"])
+        elif alg == "mmse":
+            ref = gain_ref.mmse_gains(Pw, N, p["alpha"], p["ksi_min"], p["gain_min"], p["gain_max"])
+        else:
+            Ns = gain_ref.smooth_noise(np.maximum(N, 1e-10), p["noise_mu"])
+            ref = gain_ref.omlsa_gains(Pw, Ns, p["alpha"], p["ksi_min"], p["q"], p["gain_floor"])
+        Gd = G.double().cpu().numpy().T
+        assert rel_l2(Gd, ref) < 1e-5, (alg, rel_l2(Gd, ref))
+        y = ORACLE[alg](noisy, 16000, **p)
+        sse_ref = float(np.sum((clean - np.clip(y, -1, 1)) ** 2))
+        assert abs(res["sse"][i] - sse_ref) <= 1e-5 * sse_ref, (alg, res["sse"][i], sse_ref)
+        assert res["finite"][i]
 
 
 def test_config1_ss_true_noise_10s(P):

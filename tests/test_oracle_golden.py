@@ -99,6 +99,27 @@ def test_short_hops_match_reference():
     assert n == 4 * 3 * 3 + 2 * 4
 
 
+def test_generic_shapes_match_reference():
+    """STFT shapes outside the sweep kernels' (cse_enhance_cells_generic):
+    128/32, 256/64, 512/160, 512/512, 1024/512, 2048/512, float32-stored."""
+    g = load_golden("generic_shapes_0p5s.npz")
+    noisy, clean = g["noisy"], g["clean"].astype(np.float64)
+    n = 0
+    for key in g.files:
+        if not key.startswith("y|"):
+            continue
+        alg, method, n_fft, hop = key.split("|")[1:]
+        kw = dict(CELLS[alg], n_fft=int(n_fft), hop_length=int(hop), noise_percentile=10.0,
+                  noise_method=method)
+        if method == "true_noise":
+            kw["clean_audio"] = clean
+        y = ALG[alg](noisy, 16000, **kw)
+        assert y.shape == g[key].shape, key
+        assert rel_l2(y, g[key]) < 1e-6 and rel_max(y, g[key]) < 1e-6, key
+        n += 1
+    assert n == 4 * 3 * 6
+
+
 def test_config1_ss_true_noise():
     g = load_golden("config1_ss_true_noise_10s.npz")
     clean, noisy = make_pair(0, seconds=10.0)
