@@ -210,17 +210,29 @@ def load_pmc(units_per_launch, n_fft):
     return best
 
 
+def code_text(src):
+    """C/C++/HIP source with its comments removed and whitespace runs
+    collapsed (string and character literals kept): what kernel_src_sha
+    hashes, so documentation edits leave the digest alone."""
+    import re
+    tok = re.compile(r'//[^\n]*|/\*.*?\*/|"(?:\\.|[^"\\\n])*"|\'(?:\\.|[^\'\\\n])*\'', re.S)
+    out = tok.sub(lambda m: " " if m.group(0)[0] == "/" else m.group(0), src)
+    return re.sub(r"\s+", " ", out).strip()
+
+
 def kernel_src_sha():
-    """Digest of the enhance kernel's sources and build flags: a committed PMC
-    profile counts the instructions of one binary, so bench.py uses its
-    counters only while this digest matches the one the profile recorded."""
+    """Digest of the enhance kernel's sources (code only: code_text) and build
+    flags: a committed PMC profile counts the instructions of one binary, so
+    bench.py uses its counters only while this digest matches the one the
+    profile recorded."""
     import hashlib
     import __graft_entry__ as ge
     h = hashlib.sha256()
-    for f in ("cse_enhance.hip", "cse_enhance_512.hip", "cse_enhance_1024.hip", "cse_common.hpp",
-              "cse_special.hpp"):
-        h.update(open(os.path.join(ge.CSRC, f), "rb").read())
-    h.update(open(os.path.join(REPO, "include", "cse.h"), "rb").read())
+    paths = [os.path.join(ge.CSRC, f) for f in ("cse_enhance.hip", "cse_enhance_512.hip",
+                                                 "cse_enhance_1024.hip", "cse_common.hpp",
+                                                 "cse_special.hpp")]
+    for path in paths + [os.path.join(REPO, "include", "cse.h")]:
+        h.update(code_text(open(path, encoding="utf-8").read()).encode())
     h.update(repr(sorted(ge.OWN_FLAGS.items())).encode())
     return h.hexdigest()[:16]
 

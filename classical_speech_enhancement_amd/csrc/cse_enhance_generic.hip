@@ -1,6 +1,6 @@
-// The hot path at any STFT shape the sweep kernels do not run: power-of-two
-// n_fft in [64, 2048], any hop in [1, n_fft] (e.g. 512 / 160, 1024 / 512,
-// 256 / 64, 2048 / 512).  The reference's plugins take any n_fft and
+// The hot path at any STFT shape the sweep kernels do not run: even n_fft
+// in [64, 2048], any hop in [1, n_fft] (e.g. 512 / 160, 1024 / 512, 256 / 64,
+// 2048 / 512, 400 / 160).  The reference's plugins take any n_fft and
 // hop_length (spectral_subtractor.py:6, wiener_filter.py:7, mmse.py:6,
 // advanced_mmse.py:7); its grids use 512 / 1024 at hop 128 / 256, which
 // cse_enhance_cells runs (the short hops: cse_enhance_cells_short_hop).
@@ -11,7 +11,8 @@
 //             form: gamma = max(|Y|^2 inv, eps) from the 1/max(N, eps) row,
 //             SS from N itself), the decision-directed state rr per bin in LDS
 //   irfft     x = irfft(S, n_fft) as a complex n_fft/2-point inverse FFT
-//             (radix 2, LDS) of Z_k = E_k + i O_k with
+//             (radix 2, LDS; a direct DFT when n_fft/2 is not a power of
+//             two) of Z_k = E_k + i O_k with
 //             E_k = (S_k + conj S_{M-k}) / 2, O_k = (S_k - conj S_{M-k}) W^-k / 2
 //   OLA       periodic-Hann synthesis window, overlap-add into an n_fft ring
 //   retire    the hop samples no later frame touches: divided by the window
@@ -69,7 +70,7 @@ struct GenLds {
         zi = take(4 * M);
         sr = take(4 * B);               // float S_k (re, im)
         si = take(4 * B);
-        twm = take(8 * (M / 2 > 0 ? M / 2 : 1));  // float2 e^{+2πi j/M}
+        twm = take(8 * M);              // float2 e^{+2πi j/M}
         twn = take(8 * M);              // float2 e^{+2πi k/N}
         win = take(4 * N);              // float w(n)
         rr = take(4 * B);               // float decision-directed state
@@ -120,7 +121,7 @@ __device__ void gen_cell(const Args& a, int64_t c, int N, int log2m, unsigned ch
         wsq[n] = w * w;
         ring[n] = 0.0f;
     }
-    for (int j = tid; j < M / 2; j += GEN_NT) {
+    for (int j = tid; j < M; j += GEN_NT) {
         double s, co;
         sincospi(2.0 * (double)j / (double)M, &s, &co);
         twm[j] = make_float2((float)co, (float)s);
@@ -197,11 +198,34 @@ __device__ void gen_cell(const Args& a, int64_t c, int N, int log2m, unsigned ch
             const float dr = 0.5f * (ar - br), di = 0.5f * (ai - bi);
             const float2 w = twn[k];  // W^-k = e^{+2πi k/N}
             const float orr = dr * w.x - di * w.y, oi = dr * w.y + di * w.x;
-            const int r = (int)(__brev((unsigned)k) >> (32 - log2m));
+            // radix 2: bit-reversed order; the direct DFT (log2m < 0): natural
+            const int r = log2m >= 0 ? (int)(__brev((unsigned)k) >> (32 - log2m)) : k;
             zr[r] = er - oi;  // E + i O
             zi[r] = ei + orr;
         }
         __syncthreads();
+        // M not a power of two (even n_fft such as 400): z[n] = sum_k Z_k
+        // e^{+2πi kn/M} directly into the S rows (consumed above)
+        float* xr = zr;
+        float* xi = zi;
+        if (log2m < 0) {
+            for (int n = tid; n < M; n += GEN_NT) {
+                float ar = 0.0f, ai = 0.0f;
+                int m = 0;  // k n mod M
+                for (int k = 0; k < M; ++k) {
+                    const float2 w = twm[m];
+                    ar = fmaf(zr[k], w.x, fmaf(-zi[k], w.y, ar));
+                    ai = fmaf(zr[k], w.y, fmaf(zi[k], w.x, ai));
+                    m += n;
+                    if (m >= M) m -= M;
+                }
+                sr[n] = ar;
+                si[n] = ai;
+            }
+            __syncthreads();
+            xr = sr;
+            xi = si;
+        }
         for (int s = 1; s <= log2m; ++s) {
             const int half = 1 << (s - 1);
             for (int e = tid; e < M / 2; e += GEN_NT) {
@@ -221,7 +245,7 @@ __device__ void gen_cell(const Args& a, int64_t c, int N, int log2m, unsigned ch
         // ---- window, overlap-add: x[2n] = Re z[n] / M, x[2n + 1] = Im z[n] / M
         const float inv_m = 1.0f / (float)M;
         for (int n = tid; n < N; n += GEN_NT) {
-            const float x = ((n & 1) ? zi[n >> 1] : zr[n >> 1]) * inv_m;
+            const float x = ((n & 1) ? xi[n >> 1] : xr[n >> 1]) * inv_m;
             const int ri = (int)(((int64_t)t * hop + n) % N);
             ring[ri] = fmaf(win[n], x, ring[ri]);
         }
@@ -274,8 +298,8 @@ extern "C" int cse_enhance_cells_generic(int n_fft, int64_t len, const cse_cell_
                                          float* g_out, double* sse, uint8_t* finite,
                                          cse_stream_t stream) {
     const char* name = "cse_enhance_cells_generic";
-    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 2048 && (n_fft & (n_fft - 1)) == 0,
-                  "%s: n_fft=%d (a power of two in [64, 2048])", name, n_fft);
+    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 2048 && n_fft % 2 == 0,
+                  "%s: n_fft=%d (even, in [64, 2048])", name, n_fft);
     CSE_CHECK_ARG(cells && Y && noise, "%s: NULL cells/Y/noise", name);
     CSE_CHECK_ARG(len >= 1 && len < (1ll << 40) && n_cells >= 0 && n_cells < (1ll << 31),
                   "%s: len=%lld n_cells=%lld", name, (long long)len, (long long)n_cells);
@@ -294,8 +318,9 @@ extern "C" int cse_enhance_cells_generic(int n_fft, int64_t len, const cse_cell_
     a.g_out = g_out;
     a.sse = sse;
     a.finite = finite;
-    int log2m = 0;
-    while ((2 << log2m) < n_fft) ++log2m;  // M = n_fft / 2 = 2^log2m
+    int log2m = 0;  // M = n_fft / 2 = 2^log2m; -1: M not a power of two (direct DFT)
+    while ((2 << log2m) < n_fft) ++log2m;
+    if ((2 << log2m) != n_fft) log2m = -1;
     const int bytes = GenLds(n_fft).total;
     const void* fn = (const void*)enhance_generic_kernel;
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) {

@@ -257,6 +257,50 @@ __global__ void __launch_bounds__(256) stft512_kernel(const double* __restrict__
     }
 }
 
+// Even n_fft that is not a power of two (e.g. 400, r06): the direct real DFT
+// X_k = sum_n xw[n] e^{-2πi kn/N}, fp64, one workgroup per frame, the windowed
+// frame and the N twiddles e^{-2πi m/N} in LDS (index kn mod N).  O(N B) per
+// frame where the radix-2 forms are O(N log N): the shapes the grids never use.
+constexpr int DFT_NMAX = 2048;
+__global__ void __launch_bounds__(256) stft_dft_kernel(const double* __restrict__ x,
+                                                       const double* __restrict__ x_sub,
+                                                       int64_t len, int N, int hop, int T,
+                                                       float2* __restrict__ Y,
+                                                       double* __restrict__ P) {
+    __shared__ double xw[DFT_NMAX], twr[DFT_NMAX], twi[DFT_NMAX];
+    const int t = blockIdx.x;
+    const int64_t sig = blockIdx.y;
+    const int B = N / 2 + 1;
+    const double* xs = x + sig * len;
+    const double* xd = x_sub ? x_sub + sig * len : nullptr;
+    const int64_t p0 = (int64_t)t * hop - N / 2;
+    for (int n = threadIdx.x; n < N; n += blockDim.x) {
+        double sn, c;
+        sincospi(-2.0 * (double)n / (double)N, &sn, &c);
+        twr[n] = c;
+        twi[n] = sn;
+        const int64_t si = reflect_index(p0 + n, len);
+        double v = xs[si];
+        if (xd) v = v - xd[si];
+        xw[n] = v * (0.5 - 0.5 * cospi(2.0 * (double)n / (double)N));
+    }
+    __syncthreads();
+    const int64_t row = (sig * T + t) * (int64_t)B;
+    for (int k = threadIdx.x; k < B; k += blockDim.x) {
+        double r = 0.0, i = 0.0;
+        int m = 0;  // k n mod N
+        for (int n = 0; n < N; ++n) {
+            r = fma(xw[n], twr[m], r);
+            i = fma(xw[n], twi[m], i);
+            m += k;
+            if (m >= N) m -= N;
+        }
+        if (k == 0 || k == N / 2) i = 0.0;  // pocketfft r2c: exact zero imag
+        if (Y) Y[row + k] = make_float2((float)r, (float)i);
+        if (P) P[row + k] = r * r + i * i;
+    }
+}
+
 // 1/wss for output sample o (padded position o + n_fft/2); 1 where wss <= DBL_MIN
 __global__ void istft_norm_kernel(int n_fft, int hop, int64_t len, int nf, float* out) {
     const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -284,12 +328,18 @@ extern "C" int cse_stft(const double* x, const double* x_sub, int64_t n_sig, int
     CSE_CHECK_ARG(x != nullptr, "cse_stft: x is NULL");
     CSE_CHECK_ARG(n_sig > 0 && n_sig < 65536, "cse_stft: n_sig=%lld out of range", (long long)n_sig);
     CSE_CHECK_ARG(len >= 1, "cse_stft: len=%lld", (long long)len);
-    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 2048 && (n_fft & (n_fft - 1)) == 0,
-                  "cse_stft: n_fft=%d (a power of two in [64, 2048])", n_fft);
+    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 2048 && n_fft % 2 == 0,
+                  "cse_stft: n_fft=%d (even, in [64, 2048])", n_fft);
     CSE_CHECK_ARG(hop >= 1 && hop <= n_fft, "cse_stft: hop=%d", hop);
     const int T = n_frames_for(len, hop);
     dim3 grid((unsigned)ceil_div(T, stft_fpb(n_fft)), (unsigned)n_sig);
     hipStream_t st = (hipStream_t)stream;
+    if (n_fft & (n_fft - 1)) {  // even, not a power of two: the direct DFT
+        hipLaunchKernelGGL(stft_dft_kernel, dim3((unsigned)T, (unsigned)n_sig), dim3(256), 0, st, x,
+                           x_sub, len, n_fft, hop, T, (float2*)Y, P);
+        CSE_CHECK_LAUNCH("cse_stft");
+        return CSE_OK;
+    }
     switch (n_fft) {  // 512: its own register-resident form; the rest radix 2 in LDS
         case 512:
             hipLaunchKernelGGL(stft512_kernel, dim3((unsigned)ceil_div(T, S512_FPB), (unsigned)n_sig),
@@ -322,8 +372,8 @@ extern "C" int cse_stft(const double* x, const double* x_sub, int64_t n_sig, int
 
 extern "C" int cse_istft_norm(int n_fft, int hop, int64_t len, float* out, cse_stream_t stream) {
     CSE_CHECK_ARG(out != nullptr, "cse_istft_norm: out is NULL");
-    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 2048 && (n_fft & (n_fft - 1)) == 0,
-                  "cse_istft_norm: n_fft=%d", n_fft);
+    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 2048 && n_fft % 2 == 0, "cse_istft_norm: n_fft=%d",
+                  n_fft);
     CSE_CHECK_ARG(hop >= 1 && hop <= n_fft && len >= 1, "cse_istft_norm: hop=%d len=%lld", hop,
                   (long long)len);
     const int T = n_frames_for(len, hop);

@@ -324,7 +324,8 @@ def gen_short_hops(R):
     print("short_hops_0p5s.npz", len(out))
 
 
-GENERIC_SHAPES = ((128, 32), (256, 64), (512, 160), (512, 512), (1024, 512), (2048, 512))
+GENERIC_SHAPES = ((128, 32), (256, 64), (512, 160), (512, 512), (1024, 512), (2048, 512), (400, 160),
+                  (320, 80))
 
 
 def gen_generic_shapes(R):

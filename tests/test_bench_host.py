@@ -174,3 +174,16 @@ def test_valu_prices_match_the_committed_calibration():
     assert bench.VALU_CYC <= min(mix["v_add_f32 + v_add_f32"]["8"], mix["v_fma_f32(vvv) + v_add_f32"]["8"])
     # the FP32 peak needs packed math: a scalar FMA stream reaches about half
     assert s["v_pk_fma_f32"]["tflops_8w"] > 1.8 * s["v_fma_f32"]["tflops_8w"]
+
+
+def test_kernel_digest_ignores_comments_only():
+    """kernel_src_sha hashes the code of the enhance sources (code_text):
+    comments and whitespace do not move it, code and string literals do."""
+    import bench
+    src = open(os.path.join(bench.REPO, "include", "cse.h")).read()
+    assert bench.code_text(src) == bench.code_text(src.replace("/*", "/* edited:", 1))
+    assert bench.code_text(src) == bench.code_text("// a new comment line\n" + src + "\n\n")
+    t = 'int a = 1; // c\nconst char* s = "// kept /* kept */"; /* x */ char q = \'/\';'
+    assert bench.code_text(t) == 'int a = 1; const char* s = "// kept /* kept */"; char q = \'/\';'
+    assert bench.code_text("int a = 1;") != bench.code_text("int a = 2;")
+    assert len(bench.kernel_src_sha()) == 16

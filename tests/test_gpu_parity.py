@@ -137,7 +137,7 @@ def test_short_and_sweep_hops_in_one_plan(P):
         eng.run(x, [(0, "wiener", dict(CELLS["wiener"], n_fft=1024, hop_length=2048,
                                        noise_percentile=10.0, noise_method="percentile"))])
     with pytest.raises(ValueError, match="engine supports"):
-        eng.run(x, [(0, "wiener", dict(CELLS["wiener"], n_fft=400, hop_length=160,
+        eng.run(x, [(0, "wiener", dict(CELLS["wiener"], n_fft=401, hop_length=160,
                                        noise_percentile=10.0, noise_method="percentile"))])
 
 
@@ -158,9 +158,10 @@ def test_short_hops_10s_vs_oracle(P, n_fft, hop):
 
 
 def test_generic_shapes_match_reference_golden(P):
-    """cse_enhance_cells_generic (any power-of-two n_fft in [64, 2048], any hop
-    up to n_fft; here 128/32, 256/64, 512/160, 512/512, 1024/512, 2048/512)
-    through the plugins against the reference's outputs (float32-stored)."""
+    """cse_enhance_cells_generic (any even n_fft in [64, 2048], any hop up to
+    n_fft; here 128/32, 256/64, 512/160, 512/512, 1024/512, 2048/512 and the
+    direct-DFT shapes 400/160, 320/80) through the plugins against the
+    reference's outputs (float32-stored)."""
     g = load_golden("generic_shapes_0p5s.npz")
     noisy, clean = g["noisy"], g["clean"].astype(np.float64)
     n = 0
@@ -177,10 +178,10 @@ def test_generic_shapes_match_reference_golden(P):
         assert y.shape == ref.shape, key
         assert rel_l2(y, ref) <= TOL and rel_max(y, ref) <= TOL, (key, rel_l2(y, ref))
         n += 1
-    assert n == 72
+    assert n == 96
 
 
-@pytest.mark.parametrize("n_fft,hop", [(256, 80), (512, 160), (2048, 512)])
+@pytest.mark.parametrize("n_fft,hop", [(256, 80), (512, 160), (2048, 512), (400, 160)])
 def test_generic_shapes_10s_vs_oracle(P, n_fft, hop):
     """10-s signals at generic shapes, every algorithm, against the oracle."""
     clean, noisy = make_pair(4, seconds=10.0)

@@ -101,7 +101,8 @@ def test_short_hops_match_reference():
 
 def test_generic_shapes_match_reference():
     """STFT shapes outside the sweep kernels' (cse_enhance_cells_generic):
-    128/32, 256/64, 512/160, 512/512, 1024/512, 2048/512, float32-stored."""
+    128/32, 256/64, 512/160, 512/512, 1024/512, 2048/512, 400/160 and 320/80
+    (direct DFTs), float32-stored."""
     g = load_golden("generic_shapes_0p5s.npz")
     noisy, clean = g["noisy"], g["clean"].astype(np.float64)
     n = 0
@@ -117,7 +118,7 @@ def test_generic_shapes_match_reference():
         assert y.shape == g[key].shape, key
         assert rel_l2(y, g[key]) < 1e-6 and rel_max(y, g[key]) < 1e-6, key
         n += 1
-    assert n == 4 * 3 * 6
+    assert n == 4 * 3 * 8
 
 
 def test_config1_ss_true_noise():
