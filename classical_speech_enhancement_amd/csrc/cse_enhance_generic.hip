@@ -301,7 +301,7 @@ extern "C" int cse_enhance_cells_generic(int n_fft, int64_t len, const cse_cell_
     CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 2048 && n_fft % 2 == 0,
                   "%s: n_fft=%d (even, in [64, 2048])", name, n_fft);
     CSE_CHECK_ARG(cells && Y && noise, "%s: NULL cells/Y/noise", name);
-    CSE_CHECK_ARG(len >= 1 && len < (1ll << 40) && n_cells >= 0 && n_cells < (1ll << 31),
+    CSE_CHECK_ARG(len >= 1 && len < (1ll << 30) && n_cells >= 0 && n_cells < (1ll << 31),
                   "%s: len=%lld n_cells=%lld", name, (long long)len, (long long)n_cells);
     CSE_CHECK_ARG(!y_out || (out_len >= 0 && out_len <= len), "%s: out_len=%lld not in [0, len]",
                   name, (long long)out_len);

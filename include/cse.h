@@ -298,7 +298,7 @@ int cse_enhance_cells_short_hop(int n_fft, int64_t len, const cse_cell_t* cells,
  * cell, no slot groups (cells are independent; CSE_ALGO_NONE cells are
  * skipped), a cell whose hop lies outside [1, n_fft] gets the reference's skip
  * (finite = 0, sse = NaN).  Same rows, outputs (incl. g_out) and sums as
- * cse_enhance_cells; len < 2^40.
+ * cse_enhance_cells; len < 2^30.
  */
 int cse_enhance_cells_generic(int n_fft, int64_t len, const cse_cell_t* cells, int64_t n_cells,
                               const float* Y, const float* noise, const double* clean,
