@@ -196,6 +196,21 @@ def test_generic_shapes_10s_vs_oracle(P, n_fft, hop):
         assert rel_l2(y, ref) <= TOL and rel_max(y, ref) <= TOL, (alg, rel_l2(y, ref))
 
 
+@pytest.mark.parametrize("n_fft,hop", [(400, 160), (2048, 512), (256, 64)])
+def test_noise_estimation_generic_shapes(P, n_fft, hop):
+    """plugins.noise_estimation at STFT shapes beyond the grid's (the generic
+    STFT: radix 2 or, at 400, the direct DFT) against the oracle's
+    estimators; fp32 storage of fp64 estimates, rtol 1e-6."""
+    clean, noisy = make_pair(8, seconds=2.0)
+    for method in ("percentile", "min_tracking", "true_noise"):
+        kw = dict(method=method, n_fft=n_fft, hop_length=hop, percentile=15.0,
+                  clean_audio=clean, eps=1e-10)
+        N = P.noise_estimation(noisy, 16000, **kw)
+        ref = oracle.noise_estimation(noisy, 16000, **kw)
+        assert N.shape == ref.shape, (method, N.shape, ref.shape)
+        np.testing.assert_allclose(N, ref, rtol=1e-6, atol=0, err_msg=method)
+
+
 def test_generic_gains_and_sse_match_oracle():
     """The generic kernel's gain matrices against the oracle's gain loops, and
     its SNR error sums against the oracle's (clean-scored, lag 0)."""
