@@ -308,6 +308,12 @@ def test_unknown_method_and_missing_clean_raise(P):
         P.wiener_filter(noisy, 16000, 512, 128, 0.95, 0.05, 10.0, "bogus")
     with pytest.raises(ValueError, match="TrueNoiseEstimator"):
         P.wiener_filter(noisy, 16000, 512, 128, 0.95, 0.05, 10.0, "true_noise")
+    # an odd n_fft: the reference's istft infers n_fft - 1 from the bins and
+    # rejects the longer window (librosa ParameterError); the mirror raises too
+    with pytest.raises(ValueError, match="even n_fft"):
+        P.wiener_filter(noisy, 16000, 511, 128, 0.95, 0.05, 10.0, "percentile")
+    with pytest.raises(ValueError, match="even n_fft"):
+        P.mmse(noisy, 16000, 0.98, 0.01, 0.05, 1.0, 4096, 1024, 10.0, "percentile")
 
 
 def test_gain_matrices_match_oracle_gains():
