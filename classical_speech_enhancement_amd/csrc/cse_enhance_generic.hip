@@ -1,5 +1,5 @@
 // The hot path at any STFT shape the sweep kernels do not run: even n_fft
-// in [64, 2048], any hop in [1, n_fft] (e.g. 512 / 160, 1024 / 512, 256 / 64,
+// in [64, 4096], any hop in [1, n_fft] (e.g. 512 / 160, 1024 / 512, 256 / 64,
 // 2048 / 512, 400 / 160).  The reference's plugins take any n_fft and
 // hop_length (spectral_subtractor.py:6, wiener_filter.py:7, mmse.py:6,
 // advanced_mmse.py:7); its grids use 512 / 1024 at hop 128 / 256, which
@@ -298,8 +298,8 @@ extern "C" int cse_enhance_cells_generic(int n_fft, int64_t len, const cse_cell_
                                          float* g_out, double* sse, uint8_t* finite,
                                          cse_stream_t stream) {
     const char* name = "cse_enhance_cells_generic";
-    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 2048 && n_fft % 2 == 0,
-                  "%s: n_fft=%d (even, in [64, 2048])", name, n_fft);
+    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 4096 && n_fft % 2 == 0,
+                  "%s: n_fft=%d (even, in [64, 4096])", name, n_fft);
     CSE_CHECK_ARG(cells && Y && noise, "%s: NULL cells/Y/noise", name);
     CSE_CHECK_ARG(len >= 1 && len < (1ll << 30) && n_cells >= 0 && n_cells < (1ll << 31),
                   "%s: len=%lld n_cells=%lld", name, (long long)len, (long long)n_cells);

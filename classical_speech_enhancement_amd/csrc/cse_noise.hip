@@ -704,7 +704,10 @@ __device__ __forceinline__ float rcp_rn(float x) {
 // flattened one-thread-per-bin form) ran the rows' stores at 2.5 TB/s; the
 // tiled block stores at 4.7 TB/s (tools/micro/row_store.hip).
 constexpr int FIN_F = 16;     // frames per tile
-constexpr int FIN_MAXU = 5;   // bins per thread (B <= 1,280: n_fft up to 2048, r06)
+// bins per thread: 4 (B <= 1,024: the grid's n_fft 512 / 1024 and up to 2046)
+// or 9 (B <= 2,304: n_fft up to 4096, r06), one instantiation each
+constexpr int FIN_MAXU = 4, FIN_MAXU_BIG = 9;
+template <int MAXU>
 __global__ void __launch_bounds__(256) finish_kernel(const cse_noise_job_t* __restrict__ jobs,
                                                      int B, const float* __restrict__ src,
                                                      float* __restrict__ dst) {
@@ -719,7 +722,7 @@ __global__ void __launch_bounds__(256) finish_kernel(const cse_noise_job_t* __re
     const double mu = jb.mu, c = 1.0 - mu;
     const bool inv = jb.inv_eps > 0.0;
     const float ief = (float)jb.inv_eps;
-    double st[FIN_MAXU];
+    double st[MAXU];
     for (int t0 = 0; t0 < nfr; t0 += FIN_F) {
         const int nf = min(FIN_F, nfr - t0);
         const int nld = max(0, min(nf, m - t0)) * B;  // source floats of the tile
@@ -727,7 +730,7 @@ __global__ void __launch_bounds__(256) finish_kernel(const cse_noise_job_t* __re
         for (int i = tid; i < nld; i += 256) tile[i] = Ns[(int64_t)t0 * B + i];
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < FIN_MAXU; ++u) {
+        for (int u = 0; u < MAXU; ++u) {
             const int b = tid + 256 * u;
             if (b >= B) break;
             double s = st[u];
@@ -1112,16 +1115,22 @@ extern "C" int cse_noise_finish(const cse_noise_job_t* jobs, int n_jobs, int64_t
                   "cse_noise_finish: bad arguments");
     CSE_CHECK_ARG(n_sig > 0 && n_sig < 65536 && B >= 1, "cse_noise_finish: bad shape");
     if (n_jobs == 0) return CSE_OK;
-    CSE_CHECK_ARG(B <= 256 * FIN_MAXU, "cse_noise_finish: B=%d > %d", B, 256 * FIN_MAXU);
+    CSE_CHECK_ARG(B <= 256 * FIN_MAXU_BIG, "cse_noise_finish: B=%d > %d", B, 256 * FIN_MAXU_BIG);
     const dim3 grid((unsigned)n_sig, (unsigned)n_jobs);
     const size_t lds = (size_t)FIN_F * B * 4;
-    if (lds > 65536 && hipFuncSetAttribute((const void*)finish_kernel,
+    const void* fn = B <= 256 * FIN_MAXU ? (const void*)finish_kernel<FIN_MAXU>
+                                         : (const void*)finish_kernel<FIN_MAXU_BIG>;
+    if (lds > 65536 && hipFuncSetAttribute(fn,
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds) != hipSuccess) {
         ::cse::set_error("cse_noise_finish: cannot reserve %zu bytes of LDS", lds);
         return CSE_ELAUNCH;
     }
-    hipLaunchKernelGGL(finish_kernel, grid, dim3(256), lds, (hipStream_t)stream, jobs, B, src, dst);
+    void* args[] = {&jobs, &B, &src, &dst};
+    if (hipLaunchKernel(fn, grid, dim3(256), args, lds, (hipStream_t)stream) != hipSuccess) {
+        ::cse::set_error("cse_noise_finish: launch failed");
+        return CSE_ELAUNCH;
+    }
     CSE_CHECK_LAUNCH("cse_noise_finish");
     return CSE_OK;
 }

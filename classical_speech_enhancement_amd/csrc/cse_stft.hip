@@ -27,7 +27,7 @@ __device__ __forceinline__ int64_t reflect_index(int64_t p, int64_t len) {
 // sincospi / cospi per point), and only frames that reach past either end of
 // the signal take the 64-bit reflect arithmetic.  Every element sees the same
 // operations as before, so Y and P are bit-identical to the one-frame form.
-// (n_fft 2048, r06: one frame per workgroup, the 64-KB static LDS limit)
+// (n_fft 2048 / 4096, r06: one frame per workgroup)
 constexpr int STFT_FPB = 4;
 __host__ __device__ constexpr int stft_fpb(int nfft) { return nfft > 1024 ? 1 : STFT_FPB; }
 template <int NFFT>
@@ -261,7 +261,7 @@ __global__ void __launch_bounds__(256) stft512_kernel(const double* __restrict__
 // X_k = sum_n xw[n] e^{-2πi kn/N}, fp64, one workgroup per frame, the windowed
 // frame and the N twiddles e^{-2πi m/N} in LDS (index kn mod N).  O(N B) per
 // frame where the radix-2 forms are O(N log N): the shapes the grids never use.
-constexpr int DFT_NMAX = 2048;
+constexpr int DFT_NMAX = 4096;
 __global__ void __launch_bounds__(256) stft_dft_kernel(const double* __restrict__ x,
                                                        const double* __restrict__ x_sub,
                                                        int64_t len, int N, int hop, int T,
@@ -328,8 +328,8 @@ extern "C" int cse_stft(const double* x, const double* x_sub, int64_t n_sig, int
     CSE_CHECK_ARG(x != nullptr, "cse_stft: x is NULL");
     CSE_CHECK_ARG(n_sig > 0 && n_sig < 65536, "cse_stft: n_sig=%lld out of range", (long long)n_sig);
     CSE_CHECK_ARG(len >= 1, "cse_stft: len=%lld", (long long)len);
-    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 2048 && n_fft % 2 == 0,
-                  "cse_stft: n_fft=%d (even, in [64, 2048])", n_fft);
+    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 4096 && n_fft % 2 == 0,
+                  "cse_stft: n_fft=%d (even, in [64, 4096])", n_fft);
     CSE_CHECK_ARG(hop >= 1 && hop <= n_fft, "cse_stft: hop=%d", hop);
     const int T = n_frames_for(len, hop);
     dim3 grid((unsigned)ceil_div(T, stft_fpb(n_fft)), (unsigned)n_sig);
@@ -361,8 +361,12 @@ extern "C" int cse_stft(const double* x, const double* x_sub, int64_t n_sig, int
             hipLaunchKernelGGL(stft_kernel<256>, grid, dim3(256), 0, st, x, x_sub, len, hop, T,
                                (float2*)Y, P);
             break;
-        default:  // 2048
+        case 2048:
             hipLaunchKernelGGL(stft_kernel<2048>, grid, dim3(256), 0, st, x, x_sub, len, hop, T,
+                               (float2*)Y, P);
+            break;
+        default:  // 4096
+            hipLaunchKernelGGL(stft_kernel<4096>, grid, dim3(256), 0, st, x, x_sub, len, hop, T,
                                (float2*)Y, P);
             break;
     }
@@ -372,7 +376,7 @@ extern "C" int cse_stft(const double* x, const double* x_sub, int64_t n_sig, int
 
 extern "C" int cse_istft_norm(int n_fft, int hop, int64_t len, float* out, cse_stream_t stream) {
     CSE_CHECK_ARG(out != nullptr, "cse_istft_norm: out is NULL");
-    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 2048 && n_fft % 2 == 0, "cse_istft_norm: n_fft=%d",
+    CSE_CHECK_ARG(n_fft >= 64 && n_fft <= 4096 && n_fft % 2 == 0, "cse_istft_norm: n_fft=%d",
                   n_fft);
     CSE_CHECK_ARG(hop >= 1 && hop <= n_fft && len >= 1, "cse_istft_norm: hop=%d len=%lld", hop,
                   (long long)len);

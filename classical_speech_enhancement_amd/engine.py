@@ -61,7 +61,7 @@ def _at(t, k):
 
 # hops of the sweep kernels (cse_enhance_cells) and the short hops of
 # cse_enhance_cells_short_hop, per n_fft; every other even n_fft in
-# [64, 2048] and hop in [1, n_fft] goes to cse_enhance_cells_generic
+# [64, 4096] and hop in [1, n_fft] goes to cse_enhance_cells_generic
 HOPS = (128, 256)
 SHORT_HOPS = {512: (32, 64), 1024: (64,)}
 MAIN, SHORT, GENERIC = 0, 1, 2
@@ -75,7 +75,7 @@ def route(n_fft, hop):
         return MAIN
     if hop in SHORT_HOPS.get(n_fft, ()):
         return SHORT
-    if 64 <= n_fft <= 2048 and n_fft % 2 == 0 and 1 <= hop <= n_fft:
+    if 64 <= n_fft <= 4096 and n_fft % 2 == 0 and 1 <= hop <= n_fft:
         return GENERIC
     return None
 
@@ -657,7 +657,7 @@ class MultiPlan:
             if ck not in checked:  # per distinct (algorithm, hop, n_fft, method)
                 r = route(nf, hop)
                 if r is None:
-                    raise ValueError(f"engine supports an even n_fft in [64, 2048] and "
+                    raise ValueError(f"engine supports an even n_fft in [64, 4096] and "
                                      f"hop in [1, n_fft] (got n_fft={nf}, hop={hop})")
                 if want_g and r == SHORT:
                     raise ValueError(f"gain matrices not at the short hops (n_fft={nf}, hop={hop})")

@@ -109,7 +109,7 @@ int cse_cells_per_group(int n_fft);
  * advanced_mmse.py:39 and noise_estimation.py:184-188, :136-144), computed in
  * fp64.  x: [n_sig][len] f64.  If x_sub != NULL the transform is taken of
  * (x - x_sub) (TrueNoise, noise_estimation.py:133).  T = 1 + len/hop.
- * n_fft even, in [64, 2048] (a power of two: radix 2; otherwise a direct
+ * n_fft even, in [64, 4096] (a power of two: radix 2; otherwise a direct
  * DFT), hop in [1, n_fft].
  * Outputs (either may be NULL): Y [n_sig][T][B] complex64, P [n_sig][T][B] f64 = |Y|^2.
  */
@@ -293,7 +293,7 @@ int cse_enhance_cells_short_hop(int n_fft, int64_t len, const cse_cell_t* cells,
 
 /*
  * cse_enhance_cells at any other STFT shape (r06): n_fft even, in
- * [64, 2048], cell.hop in [1, n_fft] (e.g. 512 / 160, 1024 / 512, 256 / 64,
+ * [64, 4096], cell.hop in [1, n_fft] (e.g. 512 / 160, 1024 / 512, 256 / 64,
  * 2048 / 512, 400 / 160) — the plugins' shapes beyond the grid's.  One workgroup per
  * cell, no slot groups (cells are independent; CSE_ALGO_NONE cells are
  * skipped), a cell whose hop lies outside [1, n_fft] gets the reference's skip

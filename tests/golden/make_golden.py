@@ -325,7 +325,7 @@ def gen_short_hops(R):
 
 
 GENERIC_SHAPES = ((128, 32), (256, 64), (512, 160), (512, 512), (1024, 512), (2048, 512), (400, 160),
-                  (320, 80))
+                  (320, 80), (4096, 1024))
 
 
 def gen_generic_shapes(R):

@@ -40,11 +40,11 @@ def test_version_and_error_channel(lib):
     assert b"x is NULL" in lib.cse_last_error()
     rc = lib.cse_stft(ctypes.c_void_p(16), None, 1, 100, 501, 128, None, None, None)
     assert rc == -1 and b"n_fft" in lib.cse_last_error()
-    rc = lib.cse_stft(ctypes.c_void_p(16), None, 1, 100, 4096, 128, None, None, None)
+    rc = lib.cse_stft(ctypes.c_void_p(16), None, 1, 100, 8192, 128, None, None, None)
     assert rc == -1 and b"n_fft" in lib.cse_last_error()
     args = (100, ctypes.c_void_p(16), 1, ctypes.c_void_p(16), ctypes.c_void_p(16), None, None, 0,
             None, None, None, None)
-    for bad in (32, 385, 4096):
+    for bad in (32, 385, 8192):
         rc = lib.cse_enhance_cells_generic(bad, *args)
         assert rc == -1 and b"cse_enhance_cells_generic: n_fft" in lib.cse_last_error()
     rc = lib.cse_enhance_cells(256, 100, ctypes.c_void_p(16), 1, ctypes.c_void_p(16),
@@ -126,7 +126,8 @@ def test_route_classes_pack_in_order():
     assert route(512, 128) == MAIN and route(1024, 64) == SHORT and route(512, 160) == GENERIC
     assert route(2048, 512) == GENERIC and route(1024, 512) == GENERIC
     assert route(400, 160) == GENERIC and route(500, 100) == GENERIC
-    assert route(401, 100) is None and route(4096, 1024) is None and route(256, 300) is None
+    assert route(4096, 1024) == GENERIC
+    assert route(401, 100) is None and route(8192, 1024) is None and route(256, 300) is None
 
 
 def test_cells_per_group_matches_header(lib):

@@ -178,10 +178,10 @@ def test_generic_shapes_match_reference_golden(P):
         assert y.shape == ref.shape, key
         assert rel_l2(y, ref) <= TOL and rel_max(y, ref) <= TOL, (key, rel_l2(y, ref))
         n += 1
-    assert n == 96
+    assert n == 108
 
 
-@pytest.mark.parametrize("n_fft,hop", [(256, 80), (512, 160), (2048, 512), (400, 160)])
+@pytest.mark.parametrize("n_fft,hop", [(256, 80), (512, 160), (2048, 512), (400, 160), (4096, 1024)])
 def test_generic_shapes_10s_vs_oracle(P, n_fft, hop):
     """10-s signals at generic shapes, every algorithm, against the oracle."""
     clean, noisy = make_pair(4, seconds=10.0)
@@ -196,7 +196,7 @@ def test_generic_shapes_10s_vs_oracle(P, n_fft, hop):
         assert rel_l2(y, ref) <= TOL and rel_max(y, ref) <= TOL, (alg, rel_l2(y, ref))
 
 
-@pytest.mark.parametrize("n_fft,hop", [(400, 160), (2048, 512), (256, 64)])
+@pytest.mark.parametrize("n_fft,hop", [(400, 160), (2048, 512), (256, 64), (4096, 1024)])
 def test_noise_estimation_generic_shapes(P, n_fft, hop):
     """plugins.noise_estimation at STFT shapes beyond the grid's (the generic
     STFT: radix 2 or, at 400, the direct DFT) against the oracle's
@@ -313,7 +313,7 @@ def test_unknown_method_and_missing_clean_raise(P):
     with pytest.raises(ValueError, match="even n_fft"):
         P.wiener_filter(noisy, 16000, 511, 128, 0.95, 0.05, 10.0, "percentile")
     with pytest.raises(ValueError, match="even n_fft"):
-        P.mmse(noisy, 16000, 0.98, 0.01, 0.05, 1.0, 4096, 1024, 10.0, "percentile")
+        P.mmse(noisy, 16000, 0.98, 0.01, 0.05, 1.0, 8192, 1024, 10.0, "percentile")
 
 
 def test_gain_matrices_match_oracle_gains():

@@ -118,7 +118,7 @@ def test_generic_shapes_match_reference():
         assert y.shape == g[key].shape, key
         assert rel_l2(y, g[key]) < 1e-6 and rel_max(y, g[key]) < 1e-6, key
         n += 1
-    assert n == 4 * 3 * 8
+    assert n == 4 * 3 * 9
 
 
 def test_config1_ss_true_noise():
